@@ -1,0 +1,206 @@
+"""Benchmark: Msamples/s of the path-tracing hot path, Cornell box 512x512 x 64 spp,
+depth 8 (BASELINE.json configs[1]), on N GPUs of one node.
+
+One step = one full frame: every rank renders its interleaved 64x64 tiles
+(tile id % N == rank) through libprt's HIP path into a device buffer, then the
+per-tile radiance sums are gathered to rank 0 over RCCL (torch.distributed
+'nccl' backend).  Total work is fixed as N grows ("scaling": "strong").
+
+    python bench.py --gpus 1 --steps 10 --warmup 3
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W
+
+Rank 0 prints ONE JSON line with `roofline` (trace kernel, HBM-bound
+accounting: algorithmic bytes per launch from the counted traversal work ÷ the
+kernel's average duration measured with HIP events on its stream) and
+`cpu_baseline` (the oracle port, timed on this host on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+VALU_PEAK_TFLOPS = 157.3
+# Algorithmic bytes per unit of work: one BVH node record
+# (two child boxes + refs), one triangle record (v0, e1, e2 + id), one light
+# triangle record per shadow query, the per-sample radiance write + its reduction
+# re-read, and the final per-pixel sum write.
+B_NODE, B_TRI, B_LIGHT, B_SAMPLE, B_PIXEL = 64, 48, 64, 24, 12
+# f32 operation accounting (no FMA under the parity contract): slab test of two
+# child boxes ~ 40 ops, Moller-Trumbore ~ 45 ops (with the division).
+F_NODE, F_TRI = 40, 45
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per trace launch (tools/pmc_traffic.py); null if absent")
+    return ap.parse_args()
+
+
+def cpu_baseline(flat, cam, args):
+    """Oracle (C restatement of PathTracer.trace, OpenMP) on a bounded sample of the
+    same workload: a subset of 8x8 tiles at the full spp/depth."""
+    from oracle import oracle as O
+    osc = O.OracleScene.from_flat(flat)
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    W = H = args.res
+    n_tiles_total = (W // 8) * (H // 8)
+    rng = np.random.default_rng(1)
+    perm = rng.permutation(n_tiles_total).astype(np.int32)
+    # calibrate on 4 tiles, then size the sample for ~args.cpu_seconds
+    t0 = time.perf_counter()
+    osc.render_tiles(cam, W, H, 8, 8, perm[:4], args.spp, args.depth, seed=args.seed, nthreads=cores)
+    dt = max(time.perf_counter() - t0, 1e-3)
+    n = int(min(n_tiles_total, max(8, 4 * args.cpu_seconds / dt)))
+    ids = np.sort(perm[:n])
+    t0 = time.perf_counter()
+    osc.render_tiles(cam, W, H, 8, 8, ids, args.spp, args.depth, seed=args.seed, nthreads=cores)
+    dt = time.perf_counter() - t0
+    samples = n * 64 * args.spp
+    return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "sample": f"{n} random 8x8 tiles of the {W}x{H} frame at {args.spp} spp, depth {args.depth} "
+                      f"({samples} samples, {dt:.1f} s); oracle/prt_oracle.c, reference-structure-free brute-force "
+                      f"closest hit, OpenMP"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles, tile_grid
+    from pyrenderer_amd.flatten import flatten_scene
+    from pyrenderer_amd.io_utils.read_tungsten import read_file
+
+    scene, camera = read_file(os.path.join(ROOT, "pyrenderer_amd", "media", "cornell-box", "scene.json"))
+    flat = flatten_scene(scene)
+    cam = camera.convert_to_taichi_camera().packed()
+    t_build = time.perf_counter()
+    ds = DeviceScene(flat, dev.index)
+    t_build = time.perf_counter() - t_build
+    W = H = args.res
+    T = args.tile
+    tx, ty = tile_grid(W, H, T)
+    my_tiles = interleaved_tiles(W, H, T, rank, world)
+    max_tiles = (tx * ty + world - 1) // world
+    slot_elems = T * T * 3
+    out = torch.zeros(max_tiles * slot_elems, dtype=torch.float32, device=dev)
+    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step(flags=0):
+        ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, out.data_ptr(), stream.cuda_stream,
+                               seed=args.seed, flags=flags)
+        if world > 1:
+            dist.gather(out, gather, dst=0)
+
+    # counted traversal work of one frame (deterministic: same RNG as the timed steps)
+    step(N.PRT_FLAG_STATS)
+    torch.cuda.synchronize(dev)
+    st = ds.last_stats().astype(np.float64)
+    cnt = torch.tensor(st, dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(cnt)
+    nodes, tris, ext, shadow = cnt.tolist()
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    kern_ms = 0.0
+    launches = 0
+    for _ in range(args.steps):
+        step(N.PRT_FLAG_TIME)
+        ms, nl = ds.kernel_timing()   # HIP events on `stream` around the trace kernel
+        kern_ms += ms
+        launches += nl
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_avg_ms = t.tolist()
+
+    if rank == 0:
+        samples_per_step = W * H * args.spp
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = samples_per_step / (elapsed / args.steps) / 1e6
+        # roofline of the dominant kernel (trace_kernel) on rank 0 (per launch)
+        per_rank = 1.0 / world
+        n_px_rank = len(my_tiles) * T * T
+        bytes_launch = (B_NODE * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank \
+            + B_SAMPLE * n_px_rank * args.spp + B_PIXEL * n_px_rank
+        achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
+        flops_launch = (F_NODE * 2 * nodes + F_TRI * tris) * per_rank
+        traffic = None
+        tj = args.traffic_json
+        if tj and os.path.exists(tj):
+            try:
+                d = json.load(open(tj))
+                if d.get("config") == f"{W}x{H}x{args.spp}spp_d{args.depth}" and world == 1:
+                    traffic = d.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(flat, cam, args)
+        line = {
+            "metric": "Msamples/sec Cornell box 512²×64spp at 1/2/4/8 GPU; per-pixel L2 vs CPU",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic (Cornell box scene.json)",
+            "config": {"workload": f"Cornell box {W}x{H}, {args.spp} spp, depth {args.depth}, Lambertian",
+                       "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
+                       "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "trace_kernel", "kernel_avg_ms": round(kern_avg_ms, 4),
+                         "bytes_per_launch": int(bytes_launch)},
+            "valu": {"achieved_tflops": round(flops_launch / (kern_avg_ms * 1e-3) / 1e12, 2),
+                     "peak_tflops": VALU_PEAK_TFLOPS},
+            "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),
+                                "ext_queries": round(ext / samples_per_step, 3),
+                                "shadow_queries": round(shadow / samples_per_step, 3)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,126 @@
+/*
+ * prt.h — C-ABI of libprt, the MI355X-native path-tracing core behind
+ * pyrenderer's Scene / Camera / BSDF API and core.tracing.render().
+ *
+ * The reference exposes no FFI: its hot path is the Taichi kernel closure
+ * `render()` (main_taichi.py:80-99) calling PathTracer.trace
+ * (core/tracing.py:116-155) over World.hit_all (mathematics/intersection_taichi.py:238-291),
+ * with the scene baked into Taichi fields by World.commit()
+ * (mathematics/intersection_taichi.py:220-233) and the camera by
+ * Camera.convert_to_taichi_camera() (core/camera.py:27-36).  Each entry point
+ * below names the reference interface it replaces; the Python host layer
+ * (pyrenderer_amd, ctypes) is the only caller.  INTEGRATION.md shows the
+ * binding a pyrenderer maintainer would add.
+ *
+ * Conventions: all pointers are borrowed for the duration of the call (data is
+ * copied to the device); outputs are caller-allocated, C-contiguous float32.
+ * Every int-returning function returns PRT_OK (0) or a negative PRT_ERR_*; no
+ * C++ exception crosses the ABI; prt_last_error() describes the last failure
+ * on the calling thread.  A scene handle is bound to one device and is not
+ * re-entrant; distinct handles may be driven from distinct host threads.
+ */
+#ifndef PRT_H_
+#define PRT_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRT_ABI_VERSION 1
+
+#define PRT_OK 0
+#define PRT_ERR_ARG (-1)     /* invalid argument / shape */
+#define PRT_ERR_HIP (-2)     /* HIP runtime error (no device, launch failure, ...) */
+#define PRT_ERR_OOM (-3)     /* host or device allocation failed */
+#define PRT_ERR_RCCL (-4)    /* RCCL communicator / collective failure */
+#define PRT_ERR_UNSUP (-5)   /* feature not supported by this build */
+
+/* render flags */
+#define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
+#define PRT_FLAG_TIME 0x2u   /* time the trace kernel with HIP events on its stream */
+
+/* material row (8 floats): rho.r rho.g rho.b emit sided type ior roughness */
+#define PRT_MAT_LAMBERT 0    /* core/bsdf.py:18-42 BSDFLambertian */
+#define PRT_MAT_LIGHT 1      /* core/bsdf.py:45-65 BSDFLight (emit=1, sided=1) */
+#define PRT_MAT_METAL 2      /* core/bsdf_taichi.py:45-59 */
+#define PRT_MAT_DIELECTRIC 3 /* core/bsdf_taichi.py:62-86 */
+
+/* camera record (24 floats) = CameraTaichi state (core/camera_taichi.py:10-39):
+ *   [0:16]  iview_c1..iview_c4 (rows of iview.T)
+ *   [16:20] sensor_dim = (sensor_width, sensor_height, focus_dist, aperture)
+ *   [20:24] reserved, 0 */
+#define PRT_CAM_FLOATS 24
+
+int prt_abi_version(void);
+const char* prt_last_error(void);
+/* number of visible HIP devices (0 when no GPU; returns PRT_OK either way) */
+int prt_device_count(int* n);
+
+/* ---------------------------------------------------------------- BVH ----
+ * Replaces accelerators/bvh_taichi.py:107-161 (BVH(prims).build(), median
+ * split over primitives) with a binned-SAH BVH2 over triangles.  Host only.
+ * tri_v: n_tri x 9 (v0 v1 v2).  info[6] = n_nodes, depth, n_leaves, n_tri,
+ * bits of the f32 box padding, round(SAH cost * 1000). */
+int prt_bvh_build(const float* tri_v, int64_t n_tri, int32_t max_leaf, void** out_bvh);
+int prt_bvh_info(void* bvh, int64_t* info6);
+/* nodes: n_nodes x 16 f32; tris: n_tri x 12 f32 (BVH order); order: n_tri (BVH slot -> triangle) */
+int prt_bvh_export(void* bvh, float* nodes, float* tris, int32_t* order);
+void prt_bvh_destroy(void* bvh);
+
+/* -------------------------------------------------------------- scene ----
+ * Replaces World.add / World.commit (mathematics/intersection_taichi.py:220-233)
+ * plus the Taichi fields of Quad/Cube (mathematics/shapes.py:49-57, 178-186).
+ *   tri_v   n_tri x 9 f32   world-space vertices, face order (v0 v1 v2)
+ *   tri_n   n_tri x 3 f32   face normal, reference convention (shapes.py:47,176)
+ *   tri_mat n_tri i32       material row
+ *   sph     n_sph x 4 f32   center.xyz, radius (intersection_taichi.py:15-36); n_sph may be 0
+ *   mat     n_mat x 8 f32   material rows (PRT_MAT_*)
+ *   light_tri / light_off   triangles of each emitting primitive, grouped per
+ *                           light (light_off has n_light+1 prefix offsets):
+ *                           World.sample_a_light + Quad.sample_a_point
+ *                           (intersection_taichi.py:194-207, shapes.py:62-71)
+ *   direct_rgb 3 f32        colour added when a path hits the light (tracing.py:120)
+ * Builds the BVH on the host and uploads everything to `device`. */
+int prt_scene_create(int device,
+                     const float* tri_v, const float* tri_n, const int32_t* tri_mat, int64_t n_tri,
+                     const float* sph, const int32_t* sph_mat, int64_t n_sph,
+                     const float* mat, int32_t n_mat,
+                     const int32_t* light_tri, const int32_t* light_off, int32_t n_light,
+                     const float* direct_rgb, void** out_scene);
+/* info[8] = device, n_tri, n_nodes, bvh depth, stack variant, device bytes, blocks/CU, CUs */
+int prt_scene_info(void* scene, int64_t* info8);
+void prt_scene_destroy(void* scene);
+
+/* ------------------------------------------------------------- render ----
+ * Replaces the render() kernel of main_taichi.py:80-99 run `spp` times
+ * (pixels[x,y] += PathTracer.trace(...), samples[x,y] += 1).
+ * Work = the pixels of `tile_ids` (tiles of tw x th in a W x H frame, tile id =
+ * ty * ceil(W/tw) + tx) times samples 0..spp-1, path depth `depth`.
+ * out_sum: n_tiles*tw*th x 3 f32, the per-pixel SUM of radiance over samples
+ * taken in sample order (divide by spp for the mean: pixels/samples); slot
+ * order = tile-major, then row (ly), then column (lx); pixels outside the
+ * frame are 0.  Random numbers are keyed by (seed, y*W+x, sample), so the
+ * result does not depend on the tiling or on how tiles are spread over GPUs.
+ * stats (optional, 4 x u64, needs PRT_FLAG_STATS): BVH nodes visited,
+ * triangle tests, extension queries, shadow queries. */
+int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th,
+                     const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
+                     uint32_t flags, float* out_sum, uint64_t* stats);
+/* Same work, result left in device memory `d_out_sum` (n_slots x 3 f32) and
+ * enqueued on `stream` (a hipStream_t; NULL = the scene's own stream) without
+ * a host synchronisation. tile_ids is a host array. */
+int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw, int th,
+                            const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
+                            uint32_t flags, float* d_out_sum, void* stream);
+/* trace-kernel time of the last render call made with PRT_FLAG_TIME
+ * (synchronises on its events): total ms and number of trace launches. */
+int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
+/* counters of the last render call made with PRT_FLAG_STATS (synchronises) */
+int prt_last_stats(void* scene, uint64_t* stats4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRT_H_ */

@@ -600,11 +600,18 @@ static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, in
         v3 w2 = normalize(sub(p, p2));
         float t_at = (p2.x - p.x) / w.x;
         int blocked;
-        if (cnt) cnt[3]++;
-        if (scripted) blocked = hit_all_ref(s, p, w, kTMin, t_at, rng, 1, cnt).hit;
-        else {
+        if (scripted) {
+            if (cnt) cnt[3]++;
+            blocked = hit_all_ref(s, p, w, kTMin, t_at, rng, 1, cnt).hit;
+        } else {
+            /* the shadow query is only issued when it can contribute */
             float dot1 = dot(n, w), dot2 = dot(n2, w2);
-            blocked = !(dot1 > 0.0f && dot2 > 0.0f) ? 1 : occluded(s, backend, p, w, kTMin, t_at, cnt);
+            if (dot1 > 0.0f && dot2 > 0.0f) {
+                if (cnt) cnt[3]++;
+                blocked = occluded(s, backend, p, w, kTMin, t_at, cnt);
+            } else {
+                blocked = 1;
+            }
         }
         if (!blocked) {
             float dot1 = dot(n, w), dot2 = dot(n2, w2);

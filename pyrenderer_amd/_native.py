@@ -1,0 +1,108 @@
+"""ctypes binding of libprt (include/prt.h) — the only way the product reaches the GPU.
+
+There is no CPU fallback: if libprt.so is missing or a call fails, a
+PrtError is raised with the library's message.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .build import LIB
+
+PRT_OK = 0
+PRT_FLAG_STATS = 0x1
+PRT_FLAG_TIME = 0x2
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+
+
+class PrtError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libprt error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+EXPORTS = {
+    "prt_abi_version": (_i, []),
+    "prt_last_error": (ctypes.c_char_p, []),
+    "prt_device_count": (_i, [_vp]),
+    "prt_bvh_build": (_i, [_vp, _i64, _i32, _vp]),
+    "prt_bvh_info": (_i, [_vp, _vp]),
+    "prt_bvh_export": (_i, [_vp, _vp, _vp, _vp]),
+    "prt_bvh_destroy": (None, [_vp]),
+    "prt_scene_create": (_i, [_i, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
+    "prt_scene_info": (_i, [_vp, _vp]),
+    "prt_scene_destroy": (None, [_vp]),
+    "prt_render_tiles": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
+    "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
+    "prt_kernel_timing": (_i, [_vp, _vp, _vp]),
+    "prt_last_stats": (_i, [_vp, _vp]),
+}
+
+
+def lib():
+    """Load libprt.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise PrtError(-100, f"{LIB} not found — run `python -m pyrenderer_amd.build` (hipcc, gfx950)")
+        L = ctypes.CDLL(LIB)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.prt_abi_version() != 1:
+            raise PrtError(-101, "ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != PRT_OK:
+        raise PrtError(rc, lib().prt_last_error().decode(errors="replace"))
+    return rc
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(lib().prt_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Bvh:
+    """Host BVH (prt_bvh_build): for tests / inspection; scenes build their own."""
+
+    def __init__(self, tri_v, max_leaf=4):
+        tv = np.ascontiguousarray(tri_v, np.float32).reshape(-1, 9)
+        h = _vp()
+        check(lib().prt_bvh_build(ptr(tv), tv.shape[0], max_leaf, ctypes.byref(h)))
+        self.h = h
+        info = np.zeros(6, np.int64)
+        check(lib().prt_bvh_info(self.h, ptr(info)))
+        self.n_nodes, self.depth, self.n_leaves, self.n_tri = (int(x) for x in info[:4])
+        self.pad = float(np.array([info[4]], np.int32).view(np.float32)[0])
+        self.sah_cost = info[5] / 1000.0
+
+    def export(self):
+        nodes = np.zeros((self.n_nodes, 16), np.float32)
+        tris = np.zeros((self.n_tri, 12), np.float32)
+        order = np.zeros(self.n_tri, np.int32)
+        check(lib().prt_bvh_export(self.h, ptr(nodes), ptr(tris), ptr(order)))
+        return nodes, tris, order
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().prt_bvh_destroy(self.h)
+            self.h = None

@@ -1,0 +1,95 @@
+"""Path tracing entry points (reference: core/tracing.py:47-155, main_taichi.py:80-127).
+
+`render(scene, camera, spp=..., depth=...)` is the build's `core.tracing.render()`
+(named by BASELINE.json's north star; the reference has only the Taichi
+`render()` closure of main_taichi.py:80-99).  It returns the MEAN linear
+radiance per pixel — `pixels / samples` of main_taichi.py:61-64 before the
+sqrt tone map — as float32 (W, H, 3) indexed [x][y] with y up, like the
+reference's `pixels.to_numpy()`.  Every sample runs PathTracer.trace's
+estimator in the HIP kernel (pyrenderer_amd/csrc/prt_kernels.hip).
+
+`devices=(0, 1, ...)` shards 64x64 tiles across GPUs of this process
+(tile id % n_devices); the image is bit-identical for any device count since
+random numbers are keyed by (seed, global pixel, sample).  For one process per
+GPU use pyrenderer_amd.distributed (RCCL gather over xGMI).
+"""
+import threading
+
+import numpy as np
+
+from ..device_scene import interleaved_tiles, unpack_tiles
+from ..mathematics.intersection import World
+
+
+class PathTracer:
+    """Same constructor as the reference; `trace` is per-sample GPU work, so
+    the usable entry point is `render_sums` / `render`."""
+
+    def __init__(self, world, depth, img_w, img_h):
+        self.world = world
+        self.depth = depth
+        self.img_w = img_w
+        self.img_h = img_h
+
+    def render_sums(self, cam_packed, spp, seed=0, devices=(0,), tile=64, flags=0):
+        """Per-pixel radiance SUMS over spp samples, (W, H, 3) [x][y]."""
+        W, H = self.img_w, self.img_h
+        frame = np.zeros((W, H, 3), np.float32)
+        devices = tuple(devices)
+        results = {}
+        errors = []
+
+        def run(rank, dev):
+            try:
+                ds = self.world.device_scene(dev)
+                ids = interleaved_tiles(W, H, tile, rank, len(devices))
+                sums, _ = ds.render_tiles(cam_packed, W, H, tile, tile, ids, spp, self.depth, seed, flags)
+                results[rank] = (ids, sums)
+            except Exception as e:  # surfaced below
+                errors.append(e)
+
+        if len(devices) == 1:
+            run(0, devices[0])
+        else:
+            for d in devices:
+                self.world.device_scene(d)
+            threads = [threading.Thread(target=run, args=(r, d)) for r, d in enumerate(devices)]
+            for t in threads:
+                t.start()
+            for t in threads:
+                t.join()
+        if errors:
+            raise errors[0]
+        for rank in sorted(results):
+            ids, sums = results[rank]
+            unpack_tiles(sums, W, H, tile, tile, ids, frame)
+        return frame
+
+    def render(self, cam_packed, spp, seed=0, devices=(0,), tile=64):
+        if spp <= 0:
+            return np.zeros((self.img_w, self.img_h, 3), np.float32)
+        return self.render_sums(cam_packed, spp, seed, devices, tile) / np.float32(spp)
+
+
+def build_world(scene, devices=(0,)):
+    world = World()
+    for p in scene.primitives:
+        world.add(p)
+    return world.commit(devices)
+
+
+def render(scene, camera, *, spp, depth, seed=0, resolution=None, devices=(0,), tile=64, world=None):
+    """Mean linear radiance (W, H, 3) float32, [x][y], y up.
+
+    resolution: (W, H) override of camera.resolution (the aspect ratio still
+    comes from camera.resolution, as convert_to_taichi_camera() does).
+    """
+    W, H = resolution if resolution is not None else camera.resolution
+    world = world or build_world(scene, devices)
+    tracer = PathTracer(world, depth, int(W), int(H))
+    return tracer.render(camera.convert_to_taichi_camera().packed(), spp, seed, devices, tile)
+
+
+def as_image(radiance_xy):
+    """[x][y] (y up) → [row][col] top row first, as main.py:55 writes images."""
+    return np.ascontiguousarray(np.asarray(radiance_xy).transpose(1, 0, 2)[::-1])

@@ -1,0 +1,266 @@
+// prt_bvh.cpp — host-side binned-SAH BVH2 builder over triangles.
+//
+// The reference builds its BVH over *primitives* (median split in insertion
+// order, accelerators/bvh_taichi.py:58-161) and brute-forces each primitive's
+// triangles (mathematics/shapes.py:76-110).  That does not scale past a few
+// primitives, so libprt builds a triangle-level SAH tree (the intent of the
+// reference's unused CPU builder, accelerators/bvh.py:28-215, 12 buckets) and
+// lays it out for the GPU: 64-B nodes with both child boxes, triangles as
+// (v0, e1, e2) in leaf order.  Closest-hit results do not depend on the tree:
+// ties resolve to the lowest original triangle index, which is also the
+// reference's first-found order (leaves visited in insertion order).
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "prt_internal.h"
+
+namespace prt {
+namespace {
+
+struct Box {
+    float lo[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
+    float hi[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], b.lo[k]); hi[k] = std::max(hi[k], b.hi[k]); }
+    }
+    void grow(const float* p) {
+        for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], p[k]); hi[k] = std::max(hi[k], p[k]); }
+    }
+    bool valid() const { return lo[0] <= hi[0]; }
+    double area() const {
+        if (!valid()) return 0.0;
+        double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct TNode {
+    Box box;
+    int32_t left = -1, right = -1;   // temp node ids
+    int64_t first = 0;
+    int32_t count = 0;               // > 0 for leaves
+};
+
+constexpr int kBins = 16;
+
+struct Builder {
+    const float* tv;
+    int64_t n;
+    int max_leaf;
+    std::vector<Box> tb;
+    std::vector<float> cen;    // n*3
+    std::vector<int32_t> idx;  // permutation
+    std::vector<TNode> nodes;
+    int32_t max_depth = 0;
+    int64_t leaves = 0;
+
+    int32_t build(int64_t first, int64_t count, int depth) {
+        int32_t me = (int32_t)nodes.size();
+        nodes.emplace_back();
+        Box b, cb;
+        for (int64_t i = first; i < first + count; ++i) {
+            b.grow(tb[idx[i]]);
+            cb.grow(&cen[3 * (size_t)idx[i]]);
+        }
+        nodes[me].box = b;
+        max_depth = std::max(max_depth, depth);
+        if (count <= max_leaf && (count <= 2 || depth > 40)) return make_leaf(me, first, count);
+        if (depth >= 40) {
+            // depth guard (bounds the traversal stack): object median on the widest centroid axis
+            int ax = 0;
+            for (int k = 1; k < 3; ++k)
+                if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
+            int64_t mid = first + count / 2;
+            std::nth_element(idx.begin() + first, idx.begin() + mid, idx.begin() + first + count,
+                             [&](int32_t a, int32_t c) { return cen[3 * (size_t)a + ax] < cen[3 * (size_t)c + ax]; });
+            int32_t l = build(first, mid - first, depth + 1);
+            int32_t r = build(mid, first + count - mid, depth + 1);
+            nodes[me].left = l;
+            nodes[me].right = r;
+            return me;
+        }
+        // binned SAH over the three axes
+        double best_cost = DBL_MAX;
+        int best_axis = -1, best_split = -1;
+        for (int ax = 0; ax < 3; ++ax) {
+            float ext = cb.hi[ax] - cb.lo[ax];
+            if (!(ext > 0.0f)) continue;
+            Box bins[kBins];
+            int64_t cnt[kBins] = {0};
+            double scale = kBins / (double)ext;
+            for (int64_t i = first; i < first + count; ++i) {
+                int k = (int)(((double)cen[3 * (size_t)idx[i] + ax] - cb.lo[ax]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                cnt[k]++;
+                bins[k].grow(tb[idx[i]]);
+            }
+            double ra[kBins];
+            int64_t rc[kBins];
+            Box acc;
+            int64_t c = 0;
+            for (int k = kBins - 1; k > 0; --k) {
+                acc.grow(bins[k]); c += cnt[k];
+                ra[k] = acc.area(); rc[k] = c;
+            }
+            Box lacc;
+            int64_t lc = 0;
+            for (int k = 0; k < kBins - 1; ++k) {
+                lacc.grow(bins[k]); lc += cnt[k];
+                if (lc == 0 || rc[k + 1] == 0) continue;
+                double cost = lacc.area() * (double)lc + ra[k + 1] * (double)rc[k + 1];
+                if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = k; }
+            }
+        }
+        double parent_area = b.area();
+        double leaf_cost = (double)count;
+        double split_cost = parent_area > 0.0 ? 0.5 + best_cost / parent_area : DBL_MAX;
+        if (count <= max_leaf && !(split_cost < leaf_cost)) return make_leaf(me, first, count);
+        int64_t mid;
+        if (best_axis < 0) {
+            mid = first + count / 2;  // all centroids coincide: split the range
+        } else {
+            float ext = cb.hi[best_axis] - cb.lo[best_axis];
+            double scale = kBins / (double)ext;
+            auto it = std::partition(idx.begin() + first, idx.begin() + first + count, [&](int32_t t) {
+                int k = (int)(((double)cen[3 * (size_t)t + best_axis] - cb.lo[best_axis]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                return k <= best_split;
+            });
+            mid = it - idx.begin();
+            if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        int32_t l = build(first, mid - first, depth + 1);
+        int32_t r = build(mid, first + count - mid, depth + 1);
+        nodes[me].left = l;
+        nodes[me].right = r;
+        return me;
+    }
+
+    int32_t make_leaf(int32_t me, int64_t first, int64_t count) {
+        nodes[me].first = first;
+        nodes[me].count = (int32_t)count;
+        leaves++;
+        return me;
+    }
+};
+
+inline float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
+
+}  // namespace
+
+bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, std::string* err) {
+    if (max_leaf < 1 || max_leaf > kMaxLeaf) { *err = "max_leaf must be in [1, 8]"; return false; }
+    if (n_tri < 0 || n_tri >= ((int64_t)1 << 27)) { *err = "triangle count out of range (< 2^27)"; return false; }
+    Builder B;
+    B.tv = tri_v; B.n = n_tri; B.max_leaf = max_leaf;
+    B.tb.resize((size_t)n_tri);
+    B.cen.resize((size_t)n_tri * 3);
+    B.idx.resize((size_t)n_tri);
+    Box scene;
+    float max_abs = 0.0f;
+    for (int64_t i = 0; i < n_tri; ++i) {
+        const float* t = tri_v + 9 * i;
+        Box b;
+        b.grow(t); b.grow(t + 3); b.grow(t + 6);
+        for (int k = 0; k < 9; ++k) {
+            if (!std::isfinite(t[k])) { *err = "non-finite vertex in triangle " + std::to_string(i); return false; }
+            max_abs = std::max(max_abs, std::fabs(t[k]));
+        }
+        B.tb[(size_t)i] = b;
+        for (int k = 0; k < 3; ++k) B.cen[3 * (size_t)i + k] = 0.5f * (b.lo[k] + b.hi[k]);
+        B.idx[(size_t)i] = (int32_t)i;
+        scene.grow(b);
+    }
+    float extent = scene.valid() ? std::max({scene.hi[0] - scene.lo[0], scene.hi[1] - scene.lo[1], scene.hi[2] - scene.lo[2]}) : 0.0f;
+    // Padding: ~8 ulps of the largest coordinate magnitude / extent.  Keeps the
+    // slab test conservative against Moller-Trumbore accepting hit points that
+    // lie a rounding error outside the triangle (axis-aligned Cornell edges).
+    float pad = std::max(max_abs, extent) * 1e-6f + 1e-30f;
+    int32_t root = -1;
+    if (n_tri > 0) {
+        B.nodes.reserve((size_t)(2 * n_tri / std::max(1, max_leaf / 2) + 8));
+        root = B.build(0, n_tri, 0);
+    }
+    // flatten: inner nodes in DFS preorder; leaves become child references
+    std::vector<int32_t> inner_id(B.nodes.size(), -1);
+    std::vector<int32_t> stack;
+    int32_t n_inner = 0;
+    std::vector<int32_t> preorder;
+    if (root >= 0 && B.nodes[root].count == 0) {
+        stack.push_back(root);
+        while (!stack.empty()) {
+            int32_t t = stack.back(); stack.pop_back();
+            inner_id[t] = n_inner++;
+            preorder.push_back(t);
+            const TNode& nd = B.nodes[t];
+            if (B.nodes[nd.right].count == 0) stack.push_back(nd.right);
+            if (B.nodes[nd.left].count == 0) stack.push_back(nd.left);
+        }
+    }
+    auto child_ref = [&](int32_t t) -> int32_t {
+        const TNode& c = B.nodes[t];
+        if (c.count > 0) return leaf_ref(c.first, c.count);
+        return inner_id[t];
+    };
+    auto put_box = [&](float* f, int side, const Box& bx, bool valid) {
+        float lo[3], hi[3];
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = valid ? bx.lo[k] - pad : INFINITY;
+            hi[k] = valid ? bx.hi[k] + pad : -INFINITY;
+        }
+        if (side == 0) {
+            f[0] = lo[0]; f[1] = hi[0]; f[2] = lo[1]; f[3] = hi[1]; f[4] = lo[2]; f[5] = hi[2];
+        } else {
+            f[6] = lo[0]; f[7] = hi[0]; f[8] = lo[1]; f[9] = hi[1]; f[10] = lo[2]; f[11] = hi[2];
+        }
+    };
+    out->nodes.assign((size_t)std::max<int32_t>(n_inner, 1) * 16, 0.0f);
+    if (n_inner == 0) {
+        // empty scene or a single leaf: one inner node, left = leaf (if any), right = empty
+        float* f = out->nodes.data();
+        Box empty;
+        if (root >= 0) put_box(f, 0, B.nodes[root].box, true); else put_box(f, 0, empty, false);
+        put_box(f, 1, empty, false);
+        int32_t lr = root >= 0 ? leaf_ref(0, (int)n_tri) : leaf_ref(0, 1);
+        f[12] = bits_f(lr); f[13] = bits_f(lr); f[14] = 0.0f; f[15] = 0.0f;
+        out->n_nodes = 1;
+    } else {
+        for (int32_t t : preorder) {
+            float* f = out->nodes.data() + (size_t)inner_id[t] * 16;
+            const TNode& nd = B.nodes[t];
+            put_box(f, 0, B.nodes[nd.left].box, true);
+            put_box(f, 1, B.nodes[nd.right].box, true);
+            f[12] = bits_f(child_ref(nd.left));
+            f[13] = bits_f(child_ref(nd.right));
+            f[14] = 0.0f; f[15] = 0.0f;
+        }
+        out->n_nodes = n_inner;
+    }
+    out->order = B.idx;
+    out->tris.assign((size_t)n_tri * 12, 0.0f);
+    for (int64_t s = 0; s < n_tri; ++s) {
+        int32_t o = B.idx[(size_t)s];
+        const float* t = tri_v + 9 * (int64_t)o;
+        float* d = out->tris.data() + 12 * s;
+        for (int k = 0; k < 3; ++k) {
+            d[k] = t[k];
+            d[4 + k] = t[3 + k] - t[k];   // e1 = v1 - v0 in f32 (bit-identical to on-the-fly)
+            d[8 + k] = t[6 + k] - t[k];   // e2 = v2 - v0
+        }
+        d[3] = bits_f(o); d[7] = 0.0f; d[11] = 0.0f;
+    }
+    out->depth = n_tri > 0 ? std::max(1, B.max_depth) : 1;
+    out->n_leaves = B.leaves;
+    out->pad = pad;
+    double sah = 0.0;
+    if (root >= 0 && B.nodes[root].box.area() > 0.0) {
+        double ra = B.nodes[root].box.area();
+        for (const TNode& nd : B.nodes) sah += nd.box.area() / ra * (nd.count > 0 ? (double)nd.count : 1.0);
+    }
+    out->sah_cost = sah;
+    return true;
+}
+
+}  // namespace prt

@@ -1,0 +1,388 @@
+// prt_capi.cpp — the extern "C" surface of libprt (declared in include/prt.h).
+//
+// Owns device residency of a scene (BVH, triangles, materials, lights), the
+// per-call workspaces (chunked per-sample radiance buffer, work counter), and
+// the launch sequence: memset(counter) -> trace_kernel -> reduce_kernel per
+// sample chunk, all on one stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/prt.h"
+#include "prt_internal.h"
+#include "prt_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(PRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr; bytes = 0;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
+};
+
+struct Scene {
+    int device = 0;
+    int64_t n_tri = 0;
+    int64_t n_nodes = 0;
+    int32_t depth = 0;
+    int stack = 16;
+    int n_light = 0;
+    int n_mat = 0;
+    int cus = 0;
+    int blocks_per_cu = 0;
+    float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
+    DevBuf nodes, tris, tri_nm, mats, light_v, light_off;
+    DevBuf tiles, buf, acc, work, stats;
+    hipStream_t stream = nullptr;
+    std::vector<hipEvent_t> ev;   // start/stop pairs of the last timed call
+    int ev_used = 0;
+    size_t chunk_bytes = (size_t)1 << 30;  // per-sample buffer budget
+    size_t device_bytes = 0;
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) { (void)hipGetDevice(&prev); (void)hipSetDevice(dev); }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
+    HIP_TRY(b.ensure(std::max<size_t>(bytes, 16)));
+    if (bytes) HIP_TRY(hipMemcpy(b.p, host, bytes, hipMemcpyHostToDevice));
+    *total += b.bytes;
+    return PRT_OK;
+}
+
+void destroy_scene(Scene* s) {
+    if (!s) return;
+    DeviceGuard g(s->device);
+    for (DevBuf* b : {&s->nodes, &s->tris, &s->tri_nm, &s->mats, &s->light_v, &s->light_off, &s->tiles, &s->buf,
+                      &s->acc, &s->work, &s->stats})
+        b->release();
+    for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+}
+
+int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
+                      int n_tiles, int spp, int depth) {
+    if (!s) return fail(PRT_ERR_ARG, "scene is NULL");
+    if (!cam) return fail(PRT_ERR_ARG, "cam is NULL");
+    if (W < 2 || H < 2) return fail(PRT_ERR_ARG, "W and H must be >= 2 (u = (x + r) / (W - 1))");
+    if (tw < 1 || th < 1 || (int64_t)tw * th > (1 << 20)) return fail(PRT_ERR_ARG, "bad tile size");
+    if (n_tiles < 0 || (n_tiles > 0 && !tile_ids)) return fail(PRT_ERR_ARG, "bad tile list");
+    if (spp < 0 || depth < 0) return fail(PRT_ERR_ARG, "spp and depth must be >= 0");
+    int tiles_x = (W + tw - 1) / tw, tiles_y = (H + th - 1) / th;
+    for (int i = 0; i < n_tiles; ++i)
+        if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y)
+            return fail(PRT_ERR_ARG, "tile id out of range: " + std::to_string(tile_ids[i]));
+    if ((int64_t)n_tiles * tw * th >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many pixels in one call");
+    return PRT_OK;
+}
+
+// Enqueue the whole render of a tile set on `stream`, result in d_acc.
+int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,
+                   int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc, hipStream_t stream) {
+    const int64_t n_slots = (int64_t)n_tiles * tw * th;
+    if (n_slots == 0) return PRT_OK;
+    HIP_TRY(s->tiles.ensure(sizeof(int32_t) * (size_t)n_tiles));
+    HIP_TRY(hipMemcpyAsync(s->tiles.p, tile_ids, sizeof(int32_t) * (size_t)n_tiles, hipMemcpyHostToDevice, stream));
+    if (spp == 0 || depth == 0) {
+        HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots, stream));
+        return PRT_OK;
+    }
+    int64_t per_sample = n_slots * 3 * (int64_t)sizeof(float);
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)s->chunk_bytes / per_sample));
+    // keep every chunk's item count below 2^31 (32-bit work counter)
+    chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, ((int64_t)1 << 31) / n_slots - 1));
+    HIP_TRY(s->buf.ensure((size_t)(chunk * per_sample)));
+    const bool stats = (flags & PRT_FLAG_STATS) != 0;
+    const bool timed = (flags & PRT_FLAG_TIME) != 0;
+    if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, 4 * sizeof(unsigned long long), stream));
+
+    prt::TraceParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.nodes = (const float4*)s->nodes.p;
+    P.tris = (const float4*)s->tris.p;
+    P.tri_nm = (const float4*)s->tri_nm.p;
+    P.mats = (const float*)s->mats.p;
+    P.light_v = (const float4*)s->light_v.p;
+    P.light_off = (const int*)s->light_off.p;
+    P.n_light = s->n_light;
+    P.dl_r = s->direct_rgb[0]; P.dl_g = s->direct_rgb[1]; P.dl_b = s->direct_rgb[2];
+    std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
+    P.W = W; P.H = H; P.tw = tw; P.th = th; P.tiles_x = (W + tw - 1) / tw;
+    P.tile_ids = (const int*)s->tiles.p;
+    P.n_slots = (int)n_slots;
+    P.depth = depth;
+    P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
+    P.work = (uint32_t*)s->work.p;
+    P.out = (float*)s->buf.p;
+    P.stats = (unsigned long long*)s->stats.p;
+
+    int64_t n_chunks = (spp + chunk - 1) / chunk;
+    if (timed) {
+        while ((int64_t)s->ev.size() < 2 * n_chunks) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            s->ev.push_back(e);
+        }
+        s->ev_used = (int)(2 * n_chunks);
+    } else {
+        s->ev_used = 0;
+    }
+    int k = 0;
+    for (int64_t s0 = 0; s0 < spp; s0 += chunk, ++k) {
+        int64_t n = std::min<int64_t>(chunk, spp - s0);
+        P.s0 = (int)s0;
+        P.n_items = (uint64_t)(n * n_slots);
+        int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
+        int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->blocks_per_cu * s->cus, blocks_needed));
+        HIP_TRY(hipMemsetAsync(s->work.p, 0, 16, stream));
+        if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
+        HIP_TRY(prt::launch_trace(P, s->stack, grid, stats, stream));
+        if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k + 1], stream));
+        HIP_TRY(prt::launch_reduce((const float*)s->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0, stream));
+    }
+    return PRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int prt_abi_version(void) { return PRT_ABI_VERSION; }
+
+const char* prt_last_error(void) { return g_err.c_str(); }
+
+int prt_device_count(int* n) {
+    if (!n) return fail(PRT_ERR_ARG, "n is NULL");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return PRT_OK;
+}
+
+int prt_bvh_build(const float* tri_v, int64_t n_tri, int32_t max_leaf, void** out_bvh) {
+    if (!out_bvh || (n_tri > 0 && !tri_v)) return fail(PRT_ERR_ARG, "NULL argument");
+    auto* b = new (std::nothrow) prt::BvhHost();
+    if (!b) return fail(PRT_ERR_OOM, "host allocation failed");
+    std::string err;
+    try {
+        if (!prt::build_bvh(tri_v, n_tri, max_leaf, b, &err)) { delete b; return fail(PRT_ERR_ARG, err); }
+    } catch (const std::bad_alloc&) {
+        delete b;
+        return fail(PRT_ERR_OOM, "host allocation failed during BVH build");
+    }
+    *out_bvh = b;
+    return PRT_OK;
+}
+
+int prt_bvh_info(void* bvh, int64_t* info6) {
+    auto* b = (prt::BvhHost*)bvh;
+    if (!b || !info6) return fail(PRT_ERR_ARG, "NULL argument");
+    int32_t padbits;
+    std::memcpy(&padbits, &b->pad, 4);
+    info6[0] = b->n_nodes; info6[1] = b->depth; info6[2] = b->n_leaves; info6[3] = (int64_t)b->order.size();
+    info6[4] = padbits; info6[5] = (int64_t)(b->sah_cost * 1000.0 + 0.5);
+    return PRT_OK;
+}
+
+int prt_bvh_export(void* bvh, float* nodes, float* tris, int32_t* order) {
+    auto* b = (prt::BvhHost*)bvh;
+    if (!b) return fail(PRT_ERR_ARG, "NULL argument");
+    if (nodes) std::memcpy(nodes, b->nodes.data(), sizeof(float) * b->nodes.size());
+    if (tris) std::memcpy(tris, b->tris.data(), sizeof(float) * b->tris.size());
+    if (order) std::memcpy(order, b->order.data(), sizeof(int32_t) * b->order.size());
+    return PRT_OK;
+}
+
+void prt_bvh_destroy(void* bvh) { delete (prt::BvhHost*)bvh; }
+
+int prt_scene_create(int device, const float* tri_v, const float* tri_n, const int32_t* tri_mat, int64_t n_tri,
+                     const float* sph, const int32_t* sph_mat, int64_t n_sph, const float* mat, int32_t n_mat,
+                     const int32_t* light_tri, const int32_t* light_off, int32_t n_light, const float* direct_rgb,
+                     void** out_scene) {
+    (void)sph; (void)sph_mat;
+    if (!out_scene) return fail(PRT_ERR_ARG, "out_scene is NULL");
+    *out_scene = nullptr;
+    if (n_tri < 0 || (n_tri > 0 && (!tri_v || !tri_n || !tri_mat))) return fail(PRT_ERR_ARG, "bad triangle arrays");
+    if (n_sph > 0) return fail(PRT_ERR_UNSUP, "spheres are not supported by this build yet");
+    if (n_mat < 1 || !mat) return fail(PRT_ERR_ARG, "need at least one material");
+    if (n_light < 1 || !light_off || !light_tri) return fail(PRT_ERR_ARG, "There is no lights!!! (n_light < 1)");
+    for (int64_t i = 0; i < n_tri; ++i)
+        if (tri_mat[i] < 0 || tri_mat[i] >= n_mat) return fail(PRT_ERR_ARG, "material id out of range at triangle " + std::to_string(i));
+    if (light_off[0] != 0) return fail(PRT_ERR_ARG, "light_off[0] must be 0");
+    for (int l = 0; l < n_light; ++l)
+        if (light_off[l + 1] <= light_off[l]) return fail(PRT_ERR_ARG, "every light needs >= 1 triangle");
+    for (int32_t k = 0; k < light_off[n_light]; ++k)
+        if (light_tri[k] < 0 || light_tri[k] >= n_tri) return fail(PRT_ERR_ARG, "light triangle out of range");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PRT_ERR_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(PRT_ERR_ARG, "device index out of range");
+
+    prt::BvhHost bvh;
+    std::string err;
+    try {
+        if (!prt::build_bvh(tri_v, n_tri, 4, &bvh, &err)) return fail(PRT_ERR_ARG, err);
+    } catch (const std::bad_alloc&) {
+        return fail(PRT_ERR_OOM, "host allocation failed during BVH build");
+    }
+    auto* s = new (std::nothrow) Scene();
+    if (!s) return fail(PRT_ERR_OOM, "host allocation failed");
+    s->device = device;
+    s->n_tri = n_tri;
+    s->n_nodes = bvh.n_nodes;
+    s->depth = bvh.depth;
+    s->stack = prt::stack_variant(bvh.depth);
+    s->n_light = n_light;
+    s->n_mat = n_mat;
+    if (direct_rgb) std::memcpy(s->direct_rgb, direct_rgb, sizeof(float) * 3);
+    DeviceGuard g(device);
+    int rc = PRT_OK;
+    do {
+        hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) { rc = fail(PRT_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e)); break; }
+        std::vector<float> nm((size_t)std::max<int64_t>(n_tri, 1) * 4, 0.0f);
+        for (int64_t i = 0; i < n_tri; ++i) {
+            nm[4 * i] = tri_n[3 * i]; nm[4 * i + 1] = tri_n[3 * i + 1]; nm[4 * i + 2] = tri_n[3 * i + 2];
+            nm[4 * i + 3] = bits_f(tri_mat[i]);
+        }
+        int n_lt = light_off[n_light];
+        std::vector<float> lv((size_t)n_lt * 16, 0.0f);
+        for (int k = 0; k < n_lt; ++k) {
+            int64_t t = light_tri[k];
+            for (int c = 0; c < 3; ++c) {
+                lv[16 * k + c] = tri_v[9 * t + c];
+                lv[16 * k + 4 + c] = tri_v[9 * t + 3 + c];
+                lv[16 * k + 8 + c] = tri_v[9 * t + 6 + c];
+                lv[16 * k + 12 + c] = tri_n[3 * t + c];
+            }
+            lv[16 * k + 15] = bits_f(tri_mat[t]);
+        }
+        if ((rc = upload(s->nodes, bvh.nodes.data(), sizeof(float) * bvh.nodes.size(), &s->device_bytes))) break;
+        if ((rc = upload(s->tris, bvh.tris.data(), sizeof(float) * bvh.tris.size(), &s->device_bytes))) break;
+        if ((rc = upload(s->tri_nm, nm.data(), sizeof(float) * nm.size(), &s->device_bytes))) break;
+        if ((rc = upload(s->mats, mat, sizeof(float) * 8 * (size_t)n_mat, &s->device_bytes))) break;
+        if ((rc = upload(s->light_v, lv.data(), sizeof(float) * lv.size(), &s->device_bytes))) break;
+        if ((rc = upload(s->light_off, light_off, sizeof(int32_t) * (size_t)(n_light + 1), &s->device_bytes))) break;
+        if ((e = s->work.ensure(64)) != hipSuccess || (e = s->stats.ensure(64)) != hipSuccess) {
+            rc = fail(PRT_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
+            break;
+        }
+        hipDeviceProp_t prop;
+        if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) { rc = fail(PRT_ERR_HIP, hipGetErrorString(e)); break; }
+        s->cus = prop.multiProcessorCount;
+        s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(s->stack, false));
+        if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
+    } while (0);
+    if (rc != PRT_OK) { destroy_scene(s); return rc; }
+    *out_scene = s;
+    return PRT_OK;
+}
+
+int prt_scene_info(void* scene, int64_t* info8) {
+    auto* s = (Scene*)scene;
+    if (!s || !info8) return fail(PRT_ERR_ARG, "NULL argument");
+    info8[0] = s->device; info8[1] = s->n_tri; info8[2] = s->n_nodes; info8[3] = s->depth;
+    info8[4] = s->stack; info8[5] = (int64_t)s->device_bytes; info8[6] = s->blocks_per_cu; info8[7] = s->cus;
+    return PRT_OK;
+}
+
+void prt_scene_destroy(void* scene) { destroy_scene((Scene*)scene); }
+
+int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,
+                     int spp, int depth, uint64_t seed, uint32_t flags, float* out_sum, uint64_t* stats) {
+    auto* s = (Scene*)scene;
+    int rc = check_render_args(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth);
+    if (rc) return rc;
+    if (!out_sum) return fail(PRT_ERR_ARG, "out_sum is NULL");
+    DeviceGuard g(s->device);
+    const int64_t n_slots = (int64_t)n_tiles * tw * th;
+    HIP_TRY(s->acc.ensure(std::max<size_t>(16, sizeof(float) * 3 * (size_t)n_slots)));
+    if ((rc = enqueue_render(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, (float*)s->acc.p,
+                             s->stream)))
+        return rc;
+    if (n_slots)
+        HIP_TRY(hipMemcpyAsync(out_sum, s->acc.p, sizeof(float) * 3 * (size_t)n_slots, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (stats) {
+        if (flags & PRT_FLAG_STATS) {
+            unsigned long long h[4];
+            HIP_TRY(hipMemcpy(h, s->stats.p, sizeof(h), hipMemcpyDeviceToHost));
+            for (int i = 0; i < 4; ++i) stats[i] = h[i];
+        } else {
+            std::memset(stats, 0, 4 * sizeof(uint64_t));
+        }
+    }
+    return PRT_OK;
+}
+
+int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
+                            int n_tiles, int spp, int depth, uint64_t seed, uint32_t flags, float* d_out_sum,
+                            void* stream) {
+    auto* s = (Scene*)scene;
+    int rc = check_render_args(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth);
+    if (rc) return rc;
+    if (!d_out_sum && n_tiles > 0) return fail(PRT_ERR_ARG, "d_out_sum is NULL");
+    DeviceGuard g(s->device);
+    return enqueue_render(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, d_out_sum,
+                          stream ? (hipStream_t)stream : s->stream);
+}
+
+int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
+    auto* s = (Scene*)scene;
+    if (!s || !ms_total || !launches) return fail(PRT_ERR_ARG, "NULL argument");
+    DeviceGuard g(s->device);
+    double tot = 0.0;
+    for (int k = 0; k + 1 < s->ev_used; k += 2) {
+        HIP_TRY(hipEventSynchronize(s->ev[k + 1]));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+        tot += ms;
+    }
+    *ms_total = tot;
+    *launches = s->ev_used / 2;
+    return PRT_OK;
+}
+
+int prt_last_stats(void* scene, uint64_t* stats4) {
+    auto* s = (Scene*)scene;
+    if (!s || !stats4) return fail(PRT_ERR_ARG, "NULL argument");
+    DeviceGuard g(s->device);
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long h[4];
+    HIP_TRY(hipMemcpy(h, s->stats.p, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 4; ++i) stats4[i] = h[i];
+    return PRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,37 @@
+// prt_kernels.h — launch interface of the HIP hot path (internal to libprt).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace prt {
+
+// Everything one trace launch needs, passed by value as the kernel argument.
+struct TraceParams {
+    const float4* nodes;      // BVH2, 4 float4 per node (prt_internal.h)
+    const float4* tris;       // BVH order, 3 float4 per triangle: (v0,id) (e1,0) (e2,0)
+    const float4* tri_nm;     // original order: (face normal xyz, material id bits)
+    const float* mats;        // n_mat x 8: rho.rgb, emit, sided, type, ior, roughness
+    const float4* light_v;    // per light triangle: V0, V1, V2, (normal xyz, material id bits)
+    const int* light_off;     // n_light + 1 prefix offsets into light triangles
+    int n_light;
+    float dl_r, dl_g, dl_b;   // directly-hit light colour (core/tracing.py:120)
+    float cam[24];            // packed camera (include/prt.h)
+    int W, H;                 // full frame (u = (x + r) / (W - 1))
+    int tw, th, tiles_x;      // tile geometry
+    const int* tile_ids;      // tiles of this launch
+    int n_slots;              // n_tiles * tw * th
+    int s0;                   // first sample index of this chunk
+    int depth;
+    uint32_t seed_lo, seed_hi;
+    uint64_t n_items;         // n_slots * samples in this chunk
+    uint32_t* work;           // device work counter (zeroed before the launch)
+    float* out;               // n_items x 3 radiance, item = (s - s0) * n_slots + slot
+    unsigned long long* stats;  // 4 counters (nodes, tris, ext queries, shadow queries)
+};
+
+int stack_variant(int bvh_depth);
+hipError_t launch_trace(const TraceParams& P, int stack, int grid, bool stats, hipStream_t stream);
+hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);
+int trace_blocks_per_cu(int stack, bool stats);
+
+}  // namespace prt

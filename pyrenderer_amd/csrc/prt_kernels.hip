@@ -1,0 +1,487 @@
+// prt_kernels.hip — the per-ray path-tracing hot path for CDNA4 (gfx950).
+//
+// One persistent kernel runs PathTracer.trace (reference core/tracing.py:116-155)
+// for every (pixel, sample) work item of a tile set.  Each 64-lane wave owns a
+// work queue (chunks pulled from one device counter, handed to idle lanes with
+// __ballot / popcount ranks — path regeneration), and every loop iteration runs
+// exactly ONE ray query per active lane: either a closest-hit extension ray or
+// an any-hit NEE shadow ray.  Lanes therefore stay busy across paths of
+// different length, and both query kinds share one traversal loop.
+//
+// Arithmetic contract (shared with oracle/prt_oracle.c):
+//   f32, no FMA contraction (-ffp-contract=off and the pragma below),
+//   correctly rounded '/' and sqrtf (hipcc default on gfx950), expressions in
+//   the reference's left-to-right order, the PCG stream of DESIGN.md §RNG and
+//   the minimax sin/cos of the concentric map.
+// Closest hit = minimal (t, original triangle index); the BVH only prunes.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "prt_kernels.h"
+
+namespace prt {
+namespace {
+
+constexpr float kInvPi = 0.31830988618379067154f;
+constexpr float kPiOver4 = 0.78539816339744830961f;
+constexpr float kTMin = 0.00001f;    // core/tracing.py:127
+constexpr float kTMax = 99999.9f;    // core/tracing.py:127
+constexpr float kGamma = 0x1.000006p+0f;  // f32(1 + 2*GAMMA2_3), bvh_taichi.py:179
+constexpr int kBlock = 256;
+constexpr int kChunk = 64;           // work items per queue refill (one atomic)
+
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt)
+__device__ __forceinline__ V3 normalize(V3 a) {
+    float l = sqrtf(dot(a, a));
+    return v3(a.x / l, a.y / l, a.z / l);
+}
+__device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
+
+// ------------------------------------------------------------------ RNG spec
+__device__ __forceinline__ uint32_t pcg_permute(uint32_t s) {
+    uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+    return (w >> 22u) ^ w;
+}
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) { return pcg_permute(v * 747796405u + 2891336453u); }
+__device__ __forceinline__ uint32_t rng_key(uint32_t seed_lo, uint32_t seed_hi, uint32_t pixel, uint32_t sample) {
+    uint32_t h = pcg_hash(seed_lo);
+    h = pcg_hash(h ^ seed_hi ^ pixel);
+    return pcg_hash(h + sample);
+}
+__device__ __forceinline__ float rng_next(uint32_t& st) {
+    st = st * 747796405u + 2891336453u;
+    return (float)(pcg_permute(st) >> 8) * 0x1p-24f;
+}
+// taichi_glsl randInt(a, b), inclusive
+__device__ __forceinline__ int rng_int(uint32_t& st, int a, int b) {
+    float u = rng_next(st);
+    int k = (int)floorf(u * (float)(b - a + 1));
+    k = k > b - a ? b - a : k;
+    return a + k;
+}
+
+// --------------------------------------------- concentric disk (samplers.py:9-32)
+__device__ __forceinline__ float poly_sin(float x) {
+    float z = x * x;
+    return ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x + x;
+}
+__device__ __forceinline__ float poly_cos(float x) {
+    float z = x * x;
+    return ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z
+           - 0.5f * z + 1.0f;
+}
+__device__ __forceinline__ V3 cosine_hemisphere(float u0, float u1) {
+    float ox = 2.0f * u0 - 1.0f, oy = 2.0f * u1 - 1.0f;
+    float dx = 0.0f, dy = 0.0f;
+    if (!(ox == 0.0f && oy == 0.0f)) {
+        float r, c, s;
+        if (fabsf(ox) > fabsf(oy)) {
+            r = ox;
+            float th = kPiOver4 * (oy / ox);
+            c = poly_cos(th); s = poly_sin(th);
+        } else {
+            r = oy;
+            float a = kPiOver4 * (ox / oy);   // theta = pi/2 - a
+            c = poly_sin(a); s = poly_cos(a);
+        }
+        dx = r * c; dy = r * s;
+    }
+    float m = 1.0f - dx * dx - dy * dy;
+    return v3(dx, dy, sqrtf(m > 0.0f ? m : 0.0f));
+}
+
+// rotate_z_to + rotate_vector (mat4_taichi.py:9-60): rows (x, z, n)
+__device__ __forceinline__ V3 to_world(V3 n, V3 l) {
+    V3 v = normalize(n);
+    V3 r1, r2, r3;
+    if (v.y == 1.0f) {
+        r1 = v3(1, 0, 0); r2 = v3(0, 0, 1); r3 = v3(0, 1, 0);
+    } else if (v.y == -1.0f) {
+        r1 = v3(1, 0, 0); r2 = v3(0, 0, 1); r3 = v3(0, -1, 0);
+    } else {
+        V3 x = normalize(cross(v, v3(0.0f, 1.0f, 0.0f)));
+        V3 z = normalize(cross(x, v));
+        r1 = x; r2 = z; r3 = v;
+    }
+    return normalize(r1 * l.x + r2 * l.y + r3 * l.z);
+}
+
+// ------------------------------------------------------- camera (camera_taichi.py:47-74)
+__device__ __forceinline__ void gen_ray(const float* cam, float u, float v, uint32_t& st, V3& o, V3& d) {
+    const float sd0 = cam[16], sd1 = cam[17], sd2 = cam[18], sd3 = cam[19];
+    float rd[4] = {(u - 0.5f) * sd0 / 0.5f, (v - 0.5f) * sd1 / 0.5f, -sd2, 1.0f};
+    float ro[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+    if (sd3 > 0.0f) {
+        ro[0] = sd2 * rng_next(st) - sd2 / 2.0f;
+        ro[1] = sd2 * rng_next(st) - sd2 / 2.0f;
+    }
+    float dw[4], ow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float* c = cam + 4 * i;
+        dw[i] = rd[0] * c[0] + rd[1] * c[1] + rd[2] * c[2] + rd[3] * c[3];
+        ow[i] = ro[0] * c[0] + ro[1] * c[1] + ro[2] * c[2] + ro[3] * c[3];
+    }
+    float f0 = dw[0] - ow[0], f1 = dw[1] - ow[1], f2 = dw[2] - ow[2], f3 = dw[3] - ow[3];
+    float l = sqrtf(f0 * f0 + f1 * f1 + f2 * f2 + f3 * f3);
+    o = v3(ow[0], ow[1], ow[2]);
+    d = v3(f0 / l, f1 / l, f2 / l);
+}
+
+// ---------------------------------------------------------------- traversal
+struct Counters { uint32_t nodes, tris, ext, shadow; };
+
+// Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
+__device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 o, V3 inv,
+                                     float tmin, float tmax, float& tn) {
+    float ax = (lx - o.x) * inv.x, bx = (hx - o.x) * inv.x;
+    float ay = (ly - o.y) * inv.y, by = (hy - o.y) * inv.y;
+    float az = (lz - o.z) * inv.z, bz = (hz - o.z) * inv.z;
+    float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+    float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * kGamma;
+    tfar = fminf(tfar, tmax * kGamma);
+    tn = tnear;
+    return tnear <= tfar;
+}
+
+// Moller-Trumbore in the reference's exact expression order
+// (intersection_taichi.py:69-91).  `accept(t)` decides the t-range part.
+template <bool ANY>
+__device__ __forceinline__ bool mt(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, float tbest, int id, int best_id,
+                                   float& tout) {
+    V3 c = cross(e1, d);
+    float det = dot(c, e2);
+    if (!(fabsf(det) > 0.0f)) return false;
+    float f = 1.0f / det;
+    V3 s = o - v0;
+    V3 q = cross(s, e2);
+    float t = -f * dot(q, e1);
+    bool in_range = ANY ? (t0 < t && t < tbest) : (t0 < t && (t < tbest || (t == tbest && id < best_id)));
+    if (!in_range) return false;
+    float u = -f * dot(q, d);
+    if (!(0.0f <= u && u <= 1.0f)) return false;
+    float v = f * dot(c, s);
+    if (!(v >= 0.0f && 1.0f - u - v >= 0.0f)) return false;
+    tout = t;
+    return true;
+}
+
+// Closest hit (ANY=false) or any hit (ANY=true) over the BVH2.
+// lstack: this lane's LDS stack, entry k at lstack[k * kBlock].
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool traverse(const TraceParams& P, V3 o, V3 d, float tmin, float tmax, int* lstack,
+                                         int& hit_id, float& hit_t, Counters& cn) {
+    V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float best = tmax;
+    int best_id = -1;
+    int sp = 0;
+    int cur = 0;
+    while (true) {
+        if (cur >= 0) {
+            const float4* nd = P.nodes + (size_t)cur * 4;
+            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
+            if (STATS) cn.nodes++;
+            float tl, tr;
+            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, best, tl);
+            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tmin, best, tr);
+            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
+            if (hl && hr) {
+                bool lf = tl <= tr;
+                cur = lf ? cl : cr;
+                lstack[sp * kBlock] = lf ? cr : cl;
+                ++sp;
+            } else if (hl) {
+                cur = cl;
+            } else if (hr) {
+                cur = cr;
+            } else {
+                if (sp == 0) break;
+                --sp;
+                cur = lstack[sp * kBlock];
+            }
+        } else {
+            int v = -cur - 1;
+            int first = v >> 3, cnt = (v & 7) + 1;
+            for (int k = 0; k < cnt; ++k) {
+                const float4* tp = P.tris + (size_t)(first + k) * 3;
+                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
+                int id = __float_as_int(t0.w);
+                float t;
+                if (STATS) cn.tris++;
+                if (mt<ANY>(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, t)) {
+                    best = t;
+                    best_id = id;
+                    if (ANY) { hit_id = id; hit_t = t; return true; }
+                }
+            }
+            if (sp == 0) break;
+            --sp;
+            cur = lstack[sp * kBlock];
+        }
+    }
+    hit_id = best_id;
+    hit_t = best;
+    return best_id >= 0;
+}
+
+enum : int { Q_EXT = 0, Q_SHADOW = 1 };
+
+template <int STACK, bool STATS>
+__global__ __launch_bounds__(kBlock) void trace_kernel(TraceParams P) {
+    __shared__ int s_stack[STACK * kBlock];
+    int* lstack = s_stack + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    // wave-uniform work queue [q_next, q_end)
+    uint32_t q_next = 0, q_end = 0;
+    bool exhausted = false;
+
+    // lane state
+    int item = -1;
+    int bounce = 0, qtype = Q_EXT;
+    uint32_t st = 0;
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
+    V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
+    float tmax = kTMax;
+    Counters cn = {0, 0, 0, 0};
+    const uint32_t tile_px = (uint32_t)(P.tw * P.th);
+
+    while (true) {
+        // ---------------------------------------------------------- refill
+        uint64_t idle = __ballot(item < 0);
+        for (int round = 0; round < 2 && idle; ++round) {
+            uint32_t avail = q_end - q_next;
+            if (avail == 0 && !exhausted) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(P.work, (uint32_t)kChunk);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if ((uint64_t)base >= P.n_items) {
+                    exhausted = true;
+                } else {
+                    q_next = base;
+                    q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
+                }
+                avail = q_end - q_next;
+            }
+            if (avail == 0) break;
+            uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+            uint32_t need = (uint32_t)__popcll(idle);
+            uint32_t take = need < avail ? need : avail;
+            if (((idle >> lane) & 1ull) && rank < take) {
+                item = (int)(q_next + rank);
+                // start a new sample: main_taichi.py:89-95
+                uint32_t sl = (uint32_t)item / (uint32_t)P.n_slots;
+                uint32_t slot = (uint32_t)item - sl * (uint32_t)P.n_slots;
+                uint32_t tk = slot / tile_px, loc = slot - tk * tile_px;
+                int tid = P.tile_ids[tk];
+                int x = (tid % P.tiles_x) * P.tw + (int)(loc % (uint32_t)P.tw);
+                int y = (tid / P.tiles_x) * P.th + (int)(loc / (uint32_t)P.tw);
+                L = v3(0, 0, 0);
+                if (x >= P.W || y >= P.H) {
+                    float* out = P.out + (size_t)item * 3;
+                    out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
+                    item = -2;  // served, nothing to trace this iteration
+                } else {
+                    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)P.W + (uint32_t)x, (uint32_t)P.s0 + sl);
+                    float r0 = rng_next(st);
+                    float u = ((float)x + r0) / (float)(P.W - 1);
+                    float r1 = rng_next(st);
+                    float vv = ((float)y + r1) / (float)(P.H - 1);
+                    gen_ray(P.cam, u, vv, st, o, d);
+                    beta = v3(1, 1, 1);
+                    bounce = 0;
+                    qtype = Q_EXT;
+                    tmax = kTMax;
+                }
+            }
+            q_next += take;
+            idle = __ballot(item == -1);
+        }
+        if (item == -2) item = -1;
+        if (__ballot(item >= 0) == 0) {
+            if (exhausted && q_next == q_end) break;
+            continue;
+        }
+        if (item < 0) continue;
+
+        // ------------------------------------------------------- one query
+        int hid = -1;
+        float ht = 0.0f;
+        bool hit;
+        if (qtype == Q_EXT) {
+            if (STATS) cn.ext++;
+            hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
+        } else {
+            if (STATS) cn.shadow++;
+            hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
+        }
+
+        // ------------------------------------------------- shade the result
+        bool finished = false;
+        if (qtype == Q_EXT) {
+            if (!hit) {
+                finished = true;
+            } else {
+                float4 nm = P.tri_nm[hid];
+                const float* m = P.mats + 8 * __float_as_int(nm.w);
+                V3 n = xyz(nm);
+                if (m[4] == 0.0f && dot(n, neg(d)) < 0.0f) n = neg(n);   // shapes.py:101-102
+                if (m[3] != 0.0f) {                                        // tracing.py:129-139
+                    float d1 = dot(neg(d), n);
+                    if (d1 > 0.0f) {
+                        V3 lc = v3(P.dl_r, P.dl_g, P.dl_b);
+                        L = bounce == 0 ? L + lc * beta : L + (lc * beta) * d1;
+                    }
+                    finished = true;
+                } else {
+                    // BSDFLambertian.scatter + frame (bsdf.py:29-34, shapes.py:105-108)
+                    float u0 = rng_next(st);
+                    float u1 = rng_next(st);
+                    wi = to_world(n, cosine_hemisphere(u0, u1));
+                    float pdf = fabsf(dot(n, wi)) * kInvPi;
+                    V3 p = o + d * ht;                                     // ray.at
+                    V3 att = v3(m[0], m[1], m[2]);
+                    float cw = dot(n, wi);
+                    float dz = cw > 0.0f ? cw : 0.0f;
+                    V3 nb = v3(att.x * dz / pdf * kInvPi, att.y * dz / pdf * kInvPi, att.z * dz / pdf * kInvPi);
+                    if (isnan(nb.x) || isnan(nb.y) || isnan(nb.z)) {       // tracing.py:146-148
+                        pdf = 1e-4f;
+                        nb = v3(att.x * dz / pdf * kInvPi, att.y * dz / pdf * kInvPi, att.z * dz / pdf * kInvPi);
+                    }
+                    beta = beta * nb;
+                    // sample_direct_lighting (tracing.py:92-108)
+                    int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
+                    int lo = P.light_off[li];
+                    int f = rng_int(st, 0, P.light_off[li + 1] - lo - 1);
+                    float su = sqrtf(rng_next(st));
+                    float sv = rng_next(st);
+                    float a = su * (1.0f - sv);
+                    float b = su * sv;
+                    const float4* lv = P.light_v + (size_t)(lo + f) * 4;
+                    float4 L0 = lv[0], L1 = lv[1], L2 = lv[2], LN = lv[3];
+                    float c = 1.0f - a - b;
+                    V3 p2 = (xyz(L0) * a + xyz(L1) * b) + xyz(L2) * c;
+                    V3 n2 = xyz(LN);
+                    V3 w = normalize(p2 - p);
+                    V3 w2 = normalize(p - p2);
+                    float t_at = (p2.x - p.x) / w.x;
+                    float dot1 = dot(n, w), dot2 = dot(n2, w2);
+                    o = p;
+                    if (dot1 > 0.0f && dot2 > 0.0f) {
+                        const float* em = P.mats + 8 * __float_as_int(LN.w);
+                        V3 dd = p - p2;
+                        float sl = dot(dd, dd);
+                        V3 rad = v3(em[0] * dot1 * dot2 / sl, em[1] * dot1 * dot2 / sl, em[2] * dot1 * dot2 / sl);
+                        pend = beta * rad;
+                        d = w;
+                        tmax = t_at;
+                        qtype = Q_SHADOW;
+                    } else {
+                        // no NEE term possible: go straight to the next bounce
+                        ++bounce;
+                        if (bounce >= P.depth) finished = true;
+                        d = wi;
+                        tmax = kTMax;
+                    }
+                }
+            }
+        } else {
+            if (!hit) L = L + pend;
+            ++bounce;
+            if (bounce >= P.depth) finished = true;
+            d = wi;           // o is still the hit point p
+            tmax = kTMax;
+            qtype = Q_EXT;
+        }
+        if (finished) {
+            float* out = P.out + (size_t)item * 3;
+            out[0] = L.x; out[1] = L.y; out[2] = L.z;
+            item = -1;
+        }
+    }
+    if (STATS) {
+        uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_down(a, off); b += __shfl_down(b, off);
+            c += __shfl_down(c, off); e += __shfl_down(e, off);
+        }
+        if (lane == 0) {
+            atomicAdd(P.stats + 0, (unsigned long long)a);
+            atomicAdd(P.stats + 1, (unsigned long long)b);
+            atomicAdd(P.stats + 2, (unsigned long long)c);
+            atomicAdd(P.stats + 3, (unsigned long long)e);
+        }
+    }
+}
+
+// Sequential per-pixel sum over this chunk's samples, in sample order, onto
+// the running sums (bit-identical to acc = acc + L[s] for s = 0..spp-1).
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict__ buf, float* __restrict__ acc,
+                                                        int n_slots, int n_spp, int first) {
+    int slot = blockIdx.x * kBlock + threadIdx.x;
+    if (slot >= n_slots) return;
+    float r = 0.0f, g = 0.0f, b = 0.0f;
+    if (!first) { r = acc[3 * (size_t)slot]; g = acc[3 * (size_t)slot + 1]; b = acc[3 * (size_t)slot + 2]; }
+    for (int s = 0; s < n_spp; ++s) {
+        const float* p = buf + ((size_t)s * n_slots + slot) * 3;
+        r = r + p[0]; g = g + p[1]; b = b + p[2];
+    }
+    acc[3 * (size_t)slot] = r; acc[3 * (size_t)slot + 1] = g; acc[3 * (size_t)slot + 2] = b;
+}
+
+}  // namespace
+
+template <int STACK>
+static hipError_t launch_trace_s(const TraceParams& P, int grid, bool stats, hipStream_t stream) {
+    if (stats) trace_kernel<STACK, true><<<grid, kBlock, 0, stream>>>(P);
+    else trace_kernel<STACK, false><<<grid, kBlock, 0, stream>>>(P);
+    return hipGetLastError();
+}
+
+int stack_variant(int depth) { return depth <= 16 ? 16 : depth <= 32 ? 32 : 64; }
+
+hipError_t launch_trace(const TraceParams& P, int stack, int grid, bool stats, hipStream_t stream) {
+    switch (stack) {
+        case 16: return launch_trace_s<16>(P, grid, stats, stream);
+        case 32: return launch_trace_s<32>(P, grid, stats, stream);
+        default: return launch_trace_s<64>(P, grid, stats, stream);
+    }
+}
+
+hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream) {
+    int grid = (n_slots + kBlock - 1) / kBlock;
+    reduce_kernel<<<grid, kBlock, 0, stream>>>(buf, acc, n_slots, n_spp, first ? 1 : 0);
+    return hipGetLastError();
+}
+
+template <int STACK>
+static int blocks_per_cu_s(bool stats) {
+    int n = 0;
+    if (stats) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel<STACK, true>, kBlock, 0);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel<STACK, false>, kBlock, 0);
+    return n;
+}
+
+int trace_blocks_per_cu(int stack, bool stats) {
+    switch (stack) {
+        case 16: return blocks_per_cu_s<16>(stats);
+        case 32: return blocks_per_cu_s<32>(stats);
+        default: return blocks_per_cu_s<64>(stats);
+    }
+}
+
+}  // namespace prt

@@ -1,0 +1,89 @@
+"""A flattened scene resident on one GPU (prt_scene_create / prt_render_tiles*)."""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+
+def tile_grid(W, H, tile):
+    tx = (W + tile - 1) // tile
+    ty = (H + tile - 1) // tile
+    return tx, ty
+
+
+def interleaved_tiles(W, H, tile, rank=0, world=1):
+    """Tile ids owned by `rank` of `world`: id % world == rank."""
+    tx, ty = tile_grid(W, H, tile)
+    return np.arange(rank, tx * ty, world, dtype=np.int32)
+
+
+def unpack_tiles(slots, W, H, tw, th, tile_ids, frame=None):
+    """(n_tiles*tw*th, 3) slot sums → (W, H, 3) frame indexed [x][y] (main_taichi.py:25)."""
+    tx = (W + tw - 1) // tw
+    if frame is None:
+        frame = np.zeros((W, H, 3), np.float32)
+    s = np.asarray(slots).reshape(len(tile_ids), th, tw, 3)
+    for k, tid in enumerate(np.asarray(tile_ids)):
+        x0 = (int(tid) % tx) * tw
+        y0 = (int(tid) // tx) * th
+        w = min(tw, W - x0)
+        h = min(th, H - y0)
+        frame[x0:x0 + w, y0:y0 + h] = s[k, :h, :w].transpose(1, 0, 2)
+    return frame
+
+
+class DeviceScene:
+    def __init__(self, flat, device=0):
+        self.flat = flat
+        self.device = device
+        h = ctypes.c_void_p()
+        L = N.lib()
+        sph = flat.sph if flat.sph.shape[0] else None
+        N.check(L.prt_scene_create(device, N.ptr(flat.tri_v), N.ptr(flat.tri_n), N.ptr(flat.tri_mat), flat.n_tri,
+                                   N.ptr(sph), N.ptr(flat.sph_mat if sph is not None else None),
+                                   flat.sph.shape[0], N.ptr(flat.mat), flat.mat.shape[0], N.ptr(flat.light_tri),
+                                   N.ptr(flat.light_off), flat.n_light, N.ptr(flat.direct_rgb), ctypes.byref(h)))
+        self.h = h
+        info = np.zeros(8, np.int64)
+        N.check(L.prt_scene_info(self.h, N.ptr(info)))
+        (self.device, self.n_tri, self.n_nodes, self.bvh_depth, self.stack, self.device_bytes, self.blocks_per_cu,
+         self.cus) = (int(v) for v in info)
+
+    def close(self):
+        if getattr(self, "h", None):
+            N.lib().prt_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def render_tiles(self, cam, W, H, tw, th, tile_ids, spp, depth, seed=0, flags=0):
+        """Host result: (n_tiles*tw*th, 3) per-pixel radiance sums; returns (sums, stats)."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        tile_ids = np.ascontiguousarray(tile_ids, np.int32)
+        out = np.zeros((tile_ids.shape[0] * tw * th, 3), np.float32)
+        stats = np.zeros(4, np.uint64)
+        N.check(N.lib().prt_render_tiles(self.h, N.ptr(cam), W, H, tw, th, N.ptr(tile_ids), tile_ids.shape[0], spp,
+                                         depth, int(seed), flags, N.ptr(out), N.ptr(stats)))
+        return out, stats
+
+    def render_tiles_device(self, cam, W, H, tw, th, tile_ids, spp, depth, d_out_ptr, stream_ptr=None, seed=0,
+                            flags=0):
+        """Enqueue; result stays in device memory at d_out_ptr (n_slots x 3 f32)."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        tile_ids = np.ascontiguousarray(tile_ids, np.int32)
+        N.check(N.lib().prt_render_tiles_device(self.h, N.ptr(cam), W, H, tw, th, N.ptr(tile_ids), tile_ids.shape[0],
+                                                spp, depth, int(seed), flags, ctypes.c_void_p(d_out_ptr),
+                                                ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def kernel_timing(self):
+        ms = ctypes.c_double(0.0)
+        n = ctypes.c_int64(0)
+        N.check(N.lib().prt_kernel_timing(self.h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def last_stats(self):
+        s = np.zeros(4, np.uint64)
+        N.check(N.lib().prt_last_stats(self.h, N.ptr(s)))
+        return s

@@ -1,0 +1,122 @@
+"""libprt's C-ABI: the library loads without a GPU, exports every symbol that
+include/prt.h declares, and its host-side BVH builder is sound."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "prt.h")).read()
+    return sorted(set(re.findall(r"\b(prt_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_header_symbols():
+    from pyrenderer_amd import _native as N
+    L = N.lib()
+    names = _declared()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(N.EXPORTS), set(names) ^ set(N.EXPORTS)
+    assert L.prt_abi_version() == 1
+
+
+def test_device_count_without_gpu_is_ok():
+    from pyrenderer_amd import _native as N
+    assert N.device_count() >= 0
+
+
+def test_errors_are_reported():
+    import ctypes
+    from pyrenderer_amd import _native as N
+    h = ctypes.c_void_p()
+    rc = N.lib().prt_bvh_build(None, 5, 4, ctypes.byref(h))
+    assert rc == -1 and b"NULL" in N.lib().prt_last_error()
+    with pytest.raises(N.PrtError):
+        N.Bvh(np.zeros((2, 9), np.float32), max_leaf=0)
+
+
+def _traverse_py(nodes, tris, order, ro, rd, tmin, tmax):
+    """Brute-force over the leaves reachable through conservative boxes (python)."""
+    import struct
+
+    def ref(f):
+        return struct.unpack("<i", struct.pack("<f", f))[0]
+
+    found = []
+    stack = [0]
+    inv = 1.0 / np.where(rd == 0, 1e-30, rd)
+    while stack:
+        cur = stack.pop()
+        if cur >= 0:
+            n = nodes[cur]
+            for side, c in ((0, ref(n[12])), (1, ref(n[13]))):
+                b = n[6 * side:6 * side + 6]
+                lo = np.array([b[0], b[2], b[4]])
+                hi = np.array([b[1], b[3], b[5]])
+                t0 = (lo - ro) * inv
+                t1 = (hi - ro) * inv
+                tn = np.max(np.minimum(t0, t1))
+                tf = np.min(np.maximum(t0, t1))
+                if max(tn, tmin) <= min(tf, tmax) * (1 + 1e-6):
+                    stack.append(c)
+        else:
+            v = -cur - 1
+            first, cnt = v >> 3, (v & 7) + 1
+            found.extend(order[first:first + cnt].tolist())
+    return set(found)
+
+
+def test_bvh_build_is_a_partition_with_conservative_boxes():
+    from pyrenderer_amd import _native as N
+    rng = np.random.default_rng(3)
+    n = 3000
+    c = rng.uniform(-5, 5, (n, 1, 3))
+    tv = (c + rng.normal(0, 0.2, (n, 3, 3))).astype(np.float32).reshape(n, 9)
+    b = N.Bvh(tv, max_leaf=4)
+    nodes, tris, order = b.export()
+    assert sorted(order.tolist()) == list(range(n))
+    assert 1 <= b.depth <= 64
+    # triangle records: v0 and f32 edges, original id in v0.w bits
+    np.testing.assert_array_equal(tris[:, 0:3], tv[order, 0:3])
+    np.testing.assert_array_equal(tris[:, 4:7], tv[order, 3:6] - tv[order, 0:3])
+    np.testing.assert_array_equal(tris[:, 3].view(np.int32), order)
+    # every leaf triangle lies inside the child box that references it
+    import struct
+    for nd in nodes:
+        for side in (0, 1):
+            r = struct.unpack("<i", struct.pack("<f", nd[12 + side]))[0]
+            if r < 0:
+                v = -r - 1
+                first, cnt = v >> 3, (v & 7) + 1
+                bx = nd[6 * side:6 * side + 6]
+                pts = tv[order[first:first + cnt]].reshape(-1, 3)
+                assert np.all(pts >= np.array([bx[0], bx[2], bx[4]])) and np.all(pts <= np.array([bx[1], bx[3], bx[5]]))
+    # rays: the brute-force closest triangle is among the reachable leaves
+    from oracle import oracle as O
+    osc = O.OracleScene(tv, np.tile([0, 1, 0], (n, 1)), np.zeros(n), np.arange(n), tv[:, :3], tv[:, :3],
+                        np.array([[1, 1, 1, 0, 0, 0, 1, 0]]), [0], [0, 1], [1, 1, 1])
+    ro = rng.uniform(-6, 6, (300, 3)).astype(np.float32)
+    rd = rng.normal(size=(300, 3))
+    rd = (rd / np.linalg.norm(rd, axis=1, keepdims=True)).astype(np.float32)
+    hit, t, tri, _ = osc.closest(ro, rd, 1e-5, 1e5, O.BACKEND_BRUTE)
+    assert hit.sum() > 50
+    for i in np.nonzero(hit)[0][:80]:
+        assert tri[i] in _traverse_py(nodes, tris, order, ro[i].astype(np.float64), rd[i].astype(np.float64), 1e-5, 1e5)
+
+
+def test_bvh_degenerate_inputs():
+    from pyrenderer_amd import _native as N
+    b = N.Bvh(np.zeros((0, 9), np.float32))
+    assert b.n_nodes == 1
+    one = N.Bvh(np.array([[0, 0, 0, 1, 0, 0, 0, 1, 0]], np.float32))
+    nodes, tris, order = one.export()
+    assert one.n_nodes == 1 and order.tolist() == [0]
+    same = N.Bvh(np.tile(np.array([[0, 0, 0, 1, 0, 0, 0, 1, 0]], np.float32), (50, 1)))
+    assert sorted(same.export()[2].tolist()) == list(range(50))
+    with pytest.raises(N.PrtError):
+        N.Bvh(np.full((1, 9), np.nan, np.float32))

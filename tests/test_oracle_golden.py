@@ -1,0 +1,137 @@
+"""Pin the CPU oracle (oracle/prt_oracle.c) to vectors produced by the
+reference's own code (tests/golden/*.npz; generator: tests/golden/gen/make_golden.py)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from oracle import oracle as O
+
+
+@pytest.fixture(autouse=True)
+def _spec_trig():
+    O.set_trig_mode(0)
+    yield
+    O.set_trig_mode(0)
+
+
+def test_reference_bvh_structure(oracle_scene):
+    """accelerators/bvh_taichi.py:58-161 median split / preorder / next pointers, exact."""
+    g = golden("scene_cornell.npz")
+    rb = oracle_scene.ref_bvh()
+    for k in ("obj", "left", "right", "next"):
+        np.testing.assert_array_equal(rb[k], g["bvh_" + k])
+    np.testing.assert_array_equal(rb["min"], g["bvh_min"])
+    np.testing.assert_array_equal(rb["max"], g["bvh_max"])
+
+
+@pytest.mark.parametrize("backend", [O.BACKEND_REF, O.BACKEND_BRUTE])
+def test_hit_all_bit_exact(oracle_scene, cornell, backend):
+    """World.hit_all (intersection_taichi.py:238-291): 3009 queries incl. the 9
+    recorded bounces of test.py:38-57 and 1000 shadow queries bounded by t_at_light."""
+    h = golden("hits_cornell.npz")
+    hit, t, tri, n = oracle_scene.closest(h["ro"], h["rd"], h["tmin"], h["tmax"], backend)
+    np.testing.assert_array_equal(hit, h["hit"])
+    m = hit == 1
+    np.testing.assert_array_equal(t[m], h["t"][m])
+    np.testing.assert_array_equal(n[m], h["normal"][m])
+    np.testing.assert_array_equal(cornell[2].mat[cornell[2].tri_mat[tri[m]], :3], h["rho"][m])
+
+
+def test_test_py_recorded_bounces(oracle_scene):
+    """test.py:38-57: t to the 6 printed digits, normal and albedo of all 9 segments."""
+    h = golden("hits_cornell.npz")
+    rec = h["test_py"]  # t, ro(3), rd(3), wi(3), albedo(3), normal(3)
+    hit, t, tri, n = oracle_scene.closest(rec[:, 1:4], rec[:, 4:7], 1e-5, 99999.9, O.BACKEND_REF)
+    assert hit.all()
+    np.testing.assert_allclose(t, rec[:, 0], atol=3e-6)
+    np.testing.assert_allclose(n, rec[:, 13:16], atol=1e-6)
+    # segment k+1 starts where segment k ends: ro + t*rd (6-digit print precision)
+    end = rec[:-1, 1:4] + rec[:-1, 0:1] * rec[:-1, 4:7]
+    np.testing.assert_allclose(end, rec[1:, 1:4], atol=2e-5)
+
+
+def test_moller_trumbore_kat():
+    k = golden("kats.npz")
+    for i in range(k["tri_hit"].shape[0]):
+        h, t = O.mt(k["tri_v0"][i], k["tri_v1"][i], k["tri_v2"][i], k["tri_ro"][i], k["tri_rd"][i],
+                    k["tri_t0"][i], k["tri_t1"][i])
+        assert h == k["tri_hit"][i], i
+        assert t == k["tri_t"][i] or (np.isnan(t) and np.isnan(k["tri_t"][i])), i
+
+
+def test_slab_kat():
+    k = golden("kats.npz")
+    got = [O.aabb(k["aabb_min"][i], k["aabb_max"][i], k["aabb_ro"][i], k["aabb_rd"][i], k["aabb_t0"][i],
+                  k["aabb_t1"][i]) for i in range(k["aabb_hit"].shape[0])]
+    np.testing.assert_array_equal(got, k["aabb_hit"])
+
+
+def test_samplers_kat():
+    """samplers.py:9-32 — spec polynomials vs correctly rounded cos/sin: <= 2e-7."""
+    k = golden("kats.npz")
+    d = np.array([O.disk(u) for u in k["smp_u"]])
+    h = np.array([O.hemi(u) for u in k["smp_u"]])
+    np.testing.assert_allclose(d, k["smp_disk"], atol=3e-7, rtol=0)
+    np.testing.assert_allclose(h, k["smp_hemi"], atol=2e-6, rtol=0)  # sqrt(1-r^2) amplifies near the rim
+    O.set_trig_mode(1)
+    d1 = np.array([O.disk(u) for u in k["smp_u"]])
+    np.testing.assert_array_equal(d1, k["smp_disk"])
+
+
+def test_frame_and_rotation_kat():
+    """mat4_taichi.py:9-60, bit-exact."""
+    k = golden("kats.npz")
+    fr = np.array([O.frame(n) for n in k["frm_n"]])
+    np.testing.assert_array_equal(fr, k["frm_rows"])
+    ro = np.array([O.rotate(k["frm_rows"][i], k["frm_v"][i]) for i in range(k["frm_v"].shape[0])])
+    np.testing.assert_array_equal(ro, k["frm_out"])
+
+
+def test_camera_gen_ray_kat(cornell):
+    """camera_taichi.py:47-74 on the Cornell camera, bit-exact."""
+    k = golden("kats.npz")
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    for i in range(k["cam_uv"].shape[0]):
+        o, d = O.gen_ray(cam, *k["cam_uv"][i])
+        np.testing.assert_array_equal(o, k["cam_o"][i])
+        np.testing.assert_array_equal(d, k["cam_d"][i])
+
+
+def test_sphere_and_bsdf_helpers_kat():
+    """hit_sphere (intersection_taichi.py:15-36), reflect/refract (bsdf_taichi.py:12-22) bit-exact;
+    Schlick (:6-9) within 1 ulp (the reference's pow(x, 5) vs repeated products)."""
+    k = golden("kats.npz")
+    for i in range(k["sph_hit"].shape[0]):
+        h, r = O.sphere(k["sph_c"][i], k["sph_r"][i], k["sph_o"][i], k["sph_d"][i], k["sph_t0"][i], k["sph_t1"][i])
+        assert h == k["sph_hit"][i]
+        assert r == k["sph_root"][i]
+    for i in range(k["rr_v"].shape[0]):
+        np.testing.assert_array_equal(O.reflect(k["rr_v"][i], k["rr_n"][i]), k["rr_reflect"][i])
+        np.testing.assert_array_equal(O.refract(k["rr_v"][i], k["rr_n"][i], k["rr_eta"][i]), k["rr_refract"][i])
+        assert abs(O.schlick(k["rr_cos"][i], k["rr_eta"][i]) - k["rr_schlick"][i]) <= 1.2e-7
+
+
+def test_light_sampling_kat(oracle_scene):
+    """Quad.sample_a_point (shapes.py:62-71) with scripted draws, bit-exact."""
+    k = golden("kats.npz")
+    for i in range(k["light_draws"].shape[0]):
+        p, n, e = oracle_scene.sample_light_scripted(k["light_draws"][i])
+        np.testing.assert_array_equal(p, k["light_p"][i])
+        np.testing.assert_array_equal(n, k["light_n"][i])
+        np.testing.assert_array_equal(e, k["light_e"][i])
+
+
+@pytest.mark.parametrize("depth", [4, 8])
+def test_trace_scripted_bit_exact(oracle_scene, cornell, depth):
+    """PathTracer.trace (core/tracing.py:116-155) through main_taichi.py's render()
+    body, replaying the reference's own random draws in its own order: every
+    sample's radiance AND the number of draws consumed match bit for bit."""
+    O.set_trig_mode(1)
+    tr = golden("trace_cornell.npz")
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    res = int(tr["res"])
+    for i in range(tr[f"d{depth}_color"].shape[0]):
+        x, y = tr[f"d{depth}_pixel"][i]
+        out, used = oracle_scene.trace_scripted(cam, res, res, x, y, depth, tr[f"d{depth}_streams"][i])
+        assert used == tr[f"d{depth}_used"][i], i
+        np.testing.assert_array_equal(out, tr[f"d{depth}_color"][i])
