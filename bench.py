@@ -139,17 +139,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    kern_ms = 0.0
-    launches = 0
     for _ in range(args.steps):
         step(N.PRT_FLAG_TIME)
-        ms, nl = ds.kernel_timing()   # HIP events on `stream` around the trace kernel
-        kern_ms += ms
-        launches += nl
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    kern_ms, launches = ds.kernel_timing()   # HIP events on `stream` around every trace launch
     t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -114,8 +114,9 @@ int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th
 int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw, int th,
                             const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
                             uint32_t flags, float* d_out_sum, void* stream);
-/* trace-kernel time of the last render call made with PRT_FLAG_TIME
- * (synchronises on its events): total ms and number of trace launches. */
+/* trace-kernel time of every render call made with PRT_FLAG_TIME since the
+ * previous prt_kernel_timing() (synchronises on their events, then resets):
+ * total ms and number of trace launches. */
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
 /* counters of the last render call made with PRT_FLAG_STATS (synchronises) */
 int prt_last_stats(void* scene, uint64_t* stats4);

@@ -149,17 +149,16 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.stats = (unsigned long long*)s->stats.p;
 
     int64_t n_chunks = (spp + chunk - 1) / chunk;
+    // timed launches accumulate event pairs until prt_kernel_timing() reads them
+    int k = s->ev_used / 2;
     if (timed) {
-        while ((int64_t)s->ev.size() < 2 * n_chunks) {
+        while ((int64_t)s->ev.size() < s->ev_used + 2 * n_chunks) {
             hipEvent_t e;
             HIP_TRY(hipEventCreate(&e));
             s->ev.push_back(e);
         }
-        s->ev_used = (int)(2 * n_chunks);
-    } else {
-        s->ev_used = 0;
+        s->ev_used += (int)(2 * n_chunks);
     }
-    int k = 0;
     for (int64_t s0 = 0; s0 < spp; s0 += chunk, ++k) {
         int64_t n = std::min<int64_t>(chunk, spp - s0);
         P.s0 = (int)s0;
@@ -371,6 +370,7 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
     }
     *ms_total = tot;
     *launches = s->ev_used / 2;
+    s->ev_used = 0;
     return PRT_OK;
 }
 
