@@ -98,7 +98,8 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     from pyrenderer_amd import _native as N
-    from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles, tile_grid
+    from pyrenderer_amd.device_scene import DeviceScene
+    from pyrenderer_amd.distributed import TileShard
     from pyrenderer_amd.flatten import flatten_scene
     from pyrenderer_amd.io_utils.read_tungsten import read_file
 
@@ -110,19 +111,14 @@ def main():
     t_build = time.perf_counter() - t_build
     W = H = args.res
     T = args.tile
-    tx, ty = tile_grid(W, H, T)
-    my_tiles = interleaved_tiles(W, H, T, rank, world)
-    max_tiles = (tx * ty + world - 1) // world
-    slot_elems = T * T * 3
-    out = torch.zeros(max_tiles * slot_elems, dtype=torch.float32, device=dev)
-    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    shard = TileShard(W, H, T, rank, world, dev)
+    my_tiles = shard.tiles
     stream = torch.cuda.current_stream(dev)
 
     def step(flags=0):
-        ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, out.data_ptr(), stream.cuda_stream,
-                               seed=args.seed, flags=flags)
-        if world > 1:
-            dist.gather(out, gather, dst=0)
+        ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, shard.buf.data_ptr(),
+                               stream.cuda_stream, seed=args.seed, flags=flags)
+        shard.gather()    # RCCL gather of per-tile radiance sums to rank 0
 
     # counted traversal work of one frame (deterministic: same RNG as the timed steps)
     step(N.PRT_FLAG_STATS)

@@ -40,6 +40,11 @@ extern "C" {
 /* render flags */
 #define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
 #define PRT_FLAG_TIME 0x2u   /* time the trace kernel with HIP events on its stream */
+/* trace-kernel variant in bits 8..11 (0 = automatic): 1 split closest/any-hit
+ * traversal, 2 unified traversal, 3 unified + LDS-resident scene (small scenes).
+ * All variants produce bit-identical images; the selector exists for A/B runs. */
+#define PRT_FLAG_VARIANT_SHIFT 8
+#define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFu) << PRT_FLAG_VARIANT_SHIFT)
 
 /* material row (8 floats): rho.r rho.g rho.b emit sided type ior roughness */
 #define PRT_MAT_LAMBERT 0    /* core/bsdf.py:18-42 BSDFLambertian */
@@ -120,6 +125,10 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
 /* counters of the last render call made with PRT_FLAG_STATS (synchronises) */
 int prt_last_stats(void* scene, uint64_t* stats4);
+/* diagnostic words of the same call (16 x u64): the 4 counters above, then
+ * wave-level shader clocks spent in work refill / traversal / shading, wave
+ * loop iterations, and active lanes summed over iterations */
+int prt_diag_stats(void* scene, uint64_t* stats16);
 
 #ifdef __cplusplus
 }

@@ -66,8 +66,8 @@ struct Builder {
         }
         nodes[me].box = b;
         max_depth = std::max(max_depth, depth);
-        if (count <= max_leaf && (count <= 2 || depth > 40)) return make_leaf(me, first, count);
-        if (depth >= 40) {
+        if (count <= max_leaf && (count <= 2 || depth > 32)) return make_leaf(me, first, count);
+        if (depth >= 32) {
             // depth guard (bounds the traversal stack): object median on the widest centroid axis
             int ax = 0;
             for (int k = 1; k < 3; ++k)

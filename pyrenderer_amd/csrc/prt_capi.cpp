@@ -34,6 +34,10 @@ int fail(int code, const std::string& msg) {
 
 float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
 
+// stats words: nodes, tris, ext, shadow (public) + diagnostic wave clocks
+// (refill, traversal, shading), wave iterations, active lanes at traversal
+constexpr int kStatWords = 16;
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -57,7 +61,9 @@ struct Scene {
     int n_light = 0;
     int n_mat = 0;
     int cus = 0;
-    int blocks_per_cu = 0;
+    int blocks_per_cu = 0;           // of the default variant
+    int occ[32] = {0};               // blocks/CU per (variant, stats) once queried
+    int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
     DevBuf nodes, tris, tri_nm, mats, light_v, light_off;
     DevBuf tiles, buf, acc, work, stats;
@@ -108,6 +114,11 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
     return PRT_OK;
 }
 
+// LDS-resident scene: BVH + triangles small enough to sit beside the stack
+constexpr int64_t kLdsSceneBytes = 24 * 1024;
+bool lds_fits(const Scene* s) { return 16 * (s->n_node_f4 + s->n_tri_f4) <= kLdsSceneBytes; }
+int default_variant(const Scene* s) { return lds_fits(s) ? prt::kVarWWLds6 : prt::kVarWW; }
+
 // Enqueue the whole render of a tile set on `stream`, result in d_acc.
 int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,
                    int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc, hipStream_t stream) {
@@ -126,7 +137,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     HIP_TRY(s->buf.ensure((size_t)(chunk * per_sample)));
     const bool stats = (flags & PRT_FLAG_STATS) != 0;
     const bool timed = (flags & PRT_FLAG_TIME) != 0;
-    if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, 4 * sizeof(unsigned long long), stream));
+    if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), stream));
 
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
@@ -147,6 +158,14 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.work = (uint32_t*)s->work.p;
     P.out = (float*)s->buf.p;
     P.stats = (unsigned long long*)s->stats.p;
+    P.n_node_f4 = (int)s->n_node_f4;
+    P.n_tri_f4 = (int)s->n_tri_f4;
+    int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFu);
+    if (var == 0) var = default_variant(s);
+    if (var < prt::kVarSplit || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
+    if (prt::variant_uses_lds(var) && !lds_fits(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
+    int& occ = s->occ[2 * var + (stats ? 1 : 0)];
+    if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(s->stack, var, stats, prt::trace_smem_bytes(s->stack, var, P)));
 
     int64_t n_chunks = (spp + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
@@ -164,10 +183,10 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
         P.s0 = (int)s0;
         P.n_items = (uint64_t)(n * n_slots);
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
-        int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)s->blocks_per_cu * s->cus, blocks_needed));
+        int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
         HIP_TRY(hipMemsetAsync(s->work.p, 0, 16, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
-        HIP_TRY(prt::launch_trace(P, s->stack, grid, stats, stream));
+        HIP_TRY(prt::launch_trace(P, s->stack, var, grid, stats, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k + 1], stream));
         HIP_TRY(prt::launch_reduce((const float*)s->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0, stream));
     }
@@ -251,7 +270,9 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
     prt::BvhHost bvh;
     std::string err;
     try {
-        if (!prt::build_bvh(tri_v, n_tri, 4, &bvh, &err)) return fail(PRT_ERR_ARG, err);
+        int max_leaf = 4;
+        if (const char* ml = std::getenv("PRT_MAX_LEAF")) max_leaf = std::atoi(ml);
+        if (!prt::build_bvh(tri_v, n_tri, max_leaf, &bvh, &err)) return fail(PRT_ERR_ARG, err);
     } catch (const std::bad_alloc&) {
         return fail(PRT_ERR_OOM, "host allocation failed during BVH build");
     }
@@ -293,14 +314,23 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         if ((rc = upload(s->mats, mat, sizeof(float) * 8 * (size_t)n_mat, &s->device_bytes))) break;
         if ((rc = upload(s->light_v, lv.data(), sizeof(float) * lv.size(), &s->device_bytes))) break;
         if ((rc = upload(s->light_off, light_off, sizeof(int32_t) * (size_t)(n_light + 1), &s->device_bytes))) break;
-        if ((e = s->work.ensure(64)) != hipSuccess || (e = s->stats.ensure(64)) != hipSuccess) {
+        if ((e = s->work.ensure(64)) != hipSuccess || (e = s->stats.ensure(8 * kStatWords)) != hipSuccess) {
             rc = fail(PRT_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
             break;
         }
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) { rc = fail(PRT_ERR_HIP, hipGetErrorString(e)); break; }
         s->cus = prop.multiProcessorCount;
-        s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(s->stack, false));
+        s->n_node_f4 = (int64_t)bvh.nodes.size() / 4;
+        s->n_tri_f4 = (int64_t)bvh.tris.size() / 4;
+        {
+            prt::TraceParams Q;
+            std::memset(&Q, 0, sizeof(Q));
+            Q.n_node_f4 = (int)s->n_node_f4;
+            Q.n_tri_f4 = (int)s->n_tri_f4;
+            int var = default_variant(s);
+            s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(s->stack, var, false, prt::trace_smem_bytes(s->stack, var, Q)));
+        }
         if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
     } while (0);
     if (rc != PRT_OK) { destroy_scene(s); return rc; }
@@ -382,6 +412,17 @@ int prt_last_stats(void* scene, uint64_t* stats4) {
     unsigned long long h[4];
     HIP_TRY(hipMemcpy(h, s->stats.p, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < 4; ++i) stats4[i] = h[i];
+    return PRT_OK;
+}
+
+int prt_diag_stats(void* scene, uint64_t* stats16) {
+    auto* s = (Scene*)scene;
+    if (!s || !stats16) return fail(PRT_ERR_ARG, "NULL argument");
+    DeviceGuard g(s->device);
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long h[kStatWords];
+    HIP_TRY(hipMemcpy(h, s->stats.p, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < kStatWords; ++i) stats16[i] = h[i];
     return PRT_OK;
 }
 

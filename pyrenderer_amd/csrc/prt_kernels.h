@@ -27,11 +27,25 @@ struct TraceParams {
     uint32_t* work;           // device work counter (zeroed before the launch)
     float* out;               // n_items x 3 radiance, item = (s - s0) * n_slots + slot
     unsigned long long* stats;  // 4 counters (nodes, tris, ext queries, shadow queries)
+    int n_node_f4, n_tri_f4;  // scene sizes in float4 (LDS-resident variant)
 };
 
+// trace kernel variants (A/B-able at run time through PRT_FLAG_VARIANT)
+constexpr int kVarSplit = 1;       // separate closest-hit / any-hit traversal calls (round-1 baseline)
+constexpr int kVarUnified = 2;     // one traversal loop for both query kinds
+constexpr int kVarUnifiedLds = 3;  // unified + BVH/triangles copied into LDS (small scenes)
+constexpr int kVarWW = 4;          // while-while traversal (Aila-Laine), global scene
+constexpr int kVarWWLds = 5;       // while-while + LDS-resident scene
+constexpr int kVarWWLds5 = 6;      // ... compiled for >= 5 waves per SIMD
+constexpr int kVarWWLds6 = 7;      // ... compiled for >= 6 waves per SIMD
+constexpr int kVarWW5 = 8;         // while-while, global scene, >= 5 waves per SIMD
+constexpr int kVarLast = 8;
+bool variant_uses_lds(int var);
+
 int stack_variant(int bvh_depth);
-hipError_t launch_trace(const TraceParams& P, int stack, int grid, bool stats, hipStream_t stream);
+size_t trace_smem_bytes(int stack, int var, const TraceParams& P);
+hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);
-int trace_blocks_per_cu(int stack, bool stats);
+int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 
 }  // namespace prt

@@ -237,12 +237,179 @@ __device__ __forceinline__ bool traverse(const TraceParams& P, V3 o, V3 d, float
     return best_id >= 0;
 }
 
+// Unified traversal: one loop serves closest-hit (extension) and any-hit
+// (shadow) lanes of the same wave, so the two query kinds never serialise.
+// nodes/tris point either to global memory or to the block's LDS copy of a
+// small scene (the compiler infers the address space after inlining).
+__device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, float tbest, int id, int best_id,
+                                     bool any, float& tout) {
+    V3 c = cross(e1, d);
+    float det = dot(c, e2);
+    if (!(fabsf(det) > 0.0f)) return false;
+    float f = 1.0f / det;
+    V3 s = o - v0;
+    V3 q = cross(s, e2);
+    float t = -f * dot(q, e1);
+    bool in_range = t0 < t && (t < tbest || (!any && t == tbest && id < best_id));
+    if (!in_range) return false;
+    float u = -f * dot(q, d);
+    if (!(0.0f <= u && u <= 1.0f)) return false;
+    float v = f * dot(c, s);
+    if (!(v >= 0.0f && 1.0f - u - v >= 0.0f)) return false;
+    tout = t;
+    return true;
+}
+
+template <bool STATS>
+__device__ __forceinline__ bool traverse_u(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
+                                           V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
+                                           float& hit_t, Counters& cn) {
+    V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float best = tmax;
+    int best_id = -1;
+    int sp = 0;
+    int cur = 0;
+    while (true) {
+        if (cur >= 0) {
+            const float4* nd = nodes + (size_t)cur * 4;
+            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
+            if (STATS) cn.nodes++;
+            float tl, tr;
+            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, best, tl);
+            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tmin, best, tr);
+            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
+            if (hl && hr) {
+                bool lf = tl <= tr;
+                cur = lf ? cl : cr;
+                lstack[sp * kBlock] = lf ? cr : cl;
+                ++sp;
+            } else if (hl | hr) {
+                cur = hl ? cl : cr;
+            } else {
+                if (sp == 0) break;
+                --sp;
+                cur = lstack[sp * kBlock];
+            }
+        } else {
+            int v = -cur - 1;
+            int first = v >> 3, cnt = (v & 7) + 1;
+            bool done = false;
+            for (int k = 0; k < cnt; ++k) {
+                const float4* tp = tris + (size_t)(first + k) * 3;
+                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
+                int id = __float_as_int(t0.w);
+                float t;
+                if (STATS) cn.tris++;
+                if (mt_u(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, any, t)) {
+                    best = t;
+                    best_id = id;
+                    if (any) { done = true; break; }
+                }
+            }
+            if (done || sp == 0) break;
+            --sp;
+            cur = lstack[sp * kBlock];
+        }
+    }
+    hit_id = best_id;
+    hit_t = best;
+    return best_id >= 0;
+}
+
+// While-while traversal (Aila & Laine 2009, "persistent while-while"): lanes
+// descend inner nodes until every lane of the wave holds a postponed leaf,
+// then all lanes test leaf triangles together, so inner-node and leaf work
+// of different lanes do not serialise against each other.  Stack bottom
+// holds kSentinel; leaves are negative references, inner nodes >= 0.
+constexpr int kSentinel = 0x7FFFFFFF;
+
+template <bool STATS>
+__device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
+                                            V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
+                                            float& hit_t, Counters& cn) {
+    V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    float best = tmax;
+    int best_id = -1;
+    lstack[0] = kSentinel;
+    int sp = 0;         // index of the top entry
+    int cur = 0;        // root
+    int leaf = 0;       // postponed leaf (< 0); >= 0 means none
+    do {
+        // --- inner nodes until all lanes have a postponed leaf
+        while (cur >= 0 && cur != kSentinel) {
+            const float4* nd = nodes + (size_t)cur * 4;
+            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
+            if (STATS) cn.nodes++;
+            float tl, tr;
+            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, best, tl);
+            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tmin, best, tr);
+            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
+            if (!hl && !hr) {
+                cur = lstack[sp * kBlock];
+                --sp;
+            } else {
+                bool lf = hl && (!hr || tl <= tr);
+                cur = lf ? cl : cr;
+                if (hl && hr) {
+                    ++sp;
+                    lstack[sp * kBlock] = lf ? cr : cl;
+                }
+            }
+            if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
+                leaf = cur;
+                cur = lstack[sp * kBlock];
+                --sp;
+            }
+            if (!__any(leaf >= 0)) break;  // every lane holds a leaf: go test triangles
+        }
+        // --- leaves
+        while (leaf < 0) {
+            int v = -leaf - 1;
+            int first = v >> 3, cnt = (v & 7) + 1;
+            for (int k = 0; k < cnt; ++k) {
+                const float4* tp = tris + (size_t)(first + k) * 3;
+                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
+                int id = __float_as_int(t0.w);
+                float t;
+                if (STATS) cn.tris++;
+                if (mt_u(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, any, t)) {
+                    best = t;
+                    best_id = id;
+                    if (any) { cur = kSentinel; break; }
+                }
+            }
+            if (any && best_id >= 0) { leaf = 0; break; }
+            leaf = cur;
+            if (cur < 0) {
+                cur = lstack[sp * kBlock];
+                --sp;
+            }
+        }
+    } while (cur != kSentinel || leaf < 0);
+    hit_id = best_id;
+    hit_t = best;
+    return best_id >= 0;
+}
+
 enum : int { Q_EXT = 0, Q_SHADOW = 1 };
 
-template <int STACK, bool STATS>
-__global__ __launch_bounds__(kBlock) void trace_kernel(TraceParams P) {
-    __shared__ int s_stack[STACK * kBlock];
-    int* lstack = s_stack + threadIdx.x;
+template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
+__global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
+void trace_kernel(TraceParams P) {
+    extern __shared__ float4 smem[];
+    int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
+    const float4* g_nodes = P.nodes;
+    const float4* g_tris = P.tris;
+    if (SCENE_LDS) {
+        // small scene: copy BVH + triangles into LDS once per persistent block
+        float4* sn = smem + STACK * kBlock / 4;
+        float4* st4 = sn + P.n_node_f4;
+        for (int i = threadIdx.x; i < P.n_node_f4; i += kBlock) sn[i] = P.nodes[i];
+        for (int i = threadIdx.x; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
+        __syncthreads();
+        g_nodes = sn;
+        g_tris = st4;
+    }
     const int lane = threadIdx.x & 63;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
@@ -260,7 +427,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceParams P) {
     Counters cn = {0, 0, 0, 0};
     const uint32_t tile_px = (uint32_t)(P.tw * P.th);
 
+    // diagnostic (STATS) wave-level clocks: refill / traversal / shading, iterations, active lanes
+    uint64_t c_refill = 0, c_trav = 0, c_shade = 0, n_iter = 0, n_active = 0;
+    uint64_t t_a = 0, t_b = 0;
     while (true) {
+        if (STATS) t_a = __builtin_amdgcn_s_memtime();
         // ---------------------------------------------------------- refill
         uint64_t idle = __ballot(item < 0);
         for (int round = 0; round < 2 && idle; ++round) {
@@ -322,14 +493,28 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceParams P) {
         int hid = -1;
         float ht = 0.0f;
         bool hit;
-        if (qtype == Q_EXT) {
-            if (STATS) cn.ext++;
-            hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
+        if (STATS) {
+            if (qtype == Q_EXT) cn.ext++; else cn.shadow++;
+            t_b = __builtin_amdgcn_s_memtime();
+            c_refill += t_b - t_a;
+            t_a = t_b;
+            n_iter++;
+            n_active += (uint64_t)__popcll(__ballot(true));
+        }
+        if (VAR == 0) {
+            if (qtype == Q_EXT) hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
+            else hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
+        } else if (VAR == 1) {
+            hit = traverse_u<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         } else {
-            if (STATS) cn.shadow++;
-            hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
+            hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         }
 
+        if (STATS) {
+            t_b = __builtin_amdgcn_s_memtime();
+            c_trav += t_b - t_a;
+            t_a = t_b;
+        }
         // ------------------------------------------------- shade the result
         bool finished = false;
         if (qtype == Q_EXT) {
@@ -412,6 +597,7 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceParams P) {
             out[0] = L.x; out[1] = L.y; out[2] = L.z;
             item = -1;
         }
+        if (STATS) c_shade += __builtin_amdgcn_s_memtime() - t_a;
     }
     if (STATS) {
         uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
@@ -424,6 +610,11 @@ __global__ __launch_bounds__(kBlock) void trace_kernel(TraceParams P) {
             atomicAdd(P.stats + 1, (unsigned long long)b);
             atomicAdd(P.stats + 2, (unsigned long long)c);
             atomicAdd(P.stats + 3, (unsigned long long)e);
+            atomicAdd(P.stats + 4, (unsigned long long)c_refill);
+            atomicAdd(P.stats + 5, (unsigned long long)c_trav);
+            atomicAdd(P.stats + 6, (unsigned long long)c_shade);
+            atomicAdd(P.stats + 7, (unsigned long long)n_iter);
+            atomicAdd(P.stats + 8, (unsigned long long)n_active);
         }
     }
 }
@@ -445,20 +636,51 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
 
 }  // namespace
 
-template <int STACK>
-static hipError_t launch_trace_s(const TraceParams& P, int grid, bool stats, hipStream_t stream) {
-    if (stats) trace_kernel<STACK, true><<<grid, kBlock, 0, stream>>>(P);
-    else trace_kernel<STACK, false><<<grid, kBlock, 0, stream>>>(P);
+// variant table: (traversal, LDS scene, min waves per SIMD); see prt_kernels.h
+#define PRT_VARIANTS(X)                                   \
+    X(kVarSplit, 0, false, 1)                             \
+    X(kVarUnified, 1, false, 1)                           \
+    X(kVarUnifiedLds, 1, true, 1)                         \
+    X(kVarWW, 2, false, 1)                                \
+    X(kVarWWLds, 2, true, 1)                              \
+    X(kVarWWLds5, 2, true, 5)                             \
+    X(kVarWWLds6, 2, true, 6)                             \
+    X(kVarWW5, 2, false, 5)
+
+template <int STACK, bool STATS>
+static hipError_t launch_var(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream) {
+    switch (var) {
+#define X(id, trav, lds, wpe) \
+        case id: trace_kernel<STACK, STATS, trav, lds, wpe><<<grid, kBlock, smem, stream>>>(P); break;
+        PRT_VARIANTS(X)
+#undef X
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
-int stack_variant(int depth) { return depth <= 16 ? 16 : depth <= 32 ? 32 : 64; }
+template <int STACK>
+static hipError_t launch_stack(const TraceParams& P, int var, int grid, bool stats, size_t smem, hipStream_t stream) {
+    return stats ? launch_var<STACK, true>(P, var, grid, smem, stream) : launch_var<STACK, false>(P, var, grid, smem, stream);
+}
 
-hipError_t launch_trace(const TraceParams& P, int stack, int grid, bool stats, hipStream_t stream) {
+bool variant_uses_lds(int var);
+
+// entries needed: one per level (<= depth) plus the while-while sentinel
+int stack_variant(int depth) { return depth + 1 <= 16 ? 16 : depth + 1 <= 32 ? 32 : 64; }
+
+size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
+    size_t b = (size_t)stack * kBlock * sizeof(int);
+    if (variant_uses_lds(var)) b += 16 * (size_t)(P.n_node_f4 + P.n_tri_f4);
+    return b;
+}
+
+hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream) {
+    size_t smem = trace_smem_bytes(stack, var, P);
     switch (stack) {
-        case 16: return launch_trace_s<16>(P, grid, stats, stream);
-        case 32: return launch_trace_s<32>(P, grid, stats, stream);
-        default: return launch_trace_s<64>(P, grid, stats, stream);
+        case 16: return launch_stack<16>(P, var, grid, stats, smem, stream);
+        case 32: return launch_stack<32>(P, var, grid, stats, smem, stream);
+        default: return launch_stack<64>(P, var, grid, stats, smem, stream);
     }
 }
 
@@ -468,19 +690,33 @@ hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, b
     return hipGetLastError();
 }
 
-template <int STACK>
-static int blocks_per_cu_s(bool stats) {
+template <int STACK, bool STATS>
+static int occ_var(int var, size_t smem) {
     int n = 0;
-    if (stats) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel<STACK, true>, kBlock, 0);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel<STACK, false>, kBlock, 0);
+    switch (var) {
+#define X(id, trav, lds, wpe) \
+        case id: (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel<STACK, STATS, trav, lds, wpe>, kBlock, smem); break;
+        PRT_VARIANTS(X)
+#undef X
+        default: break;
+    }
     return n;
 }
 
-int trace_blocks_per_cu(int stack, bool stats) {
+bool variant_uses_lds(int var) {
+    switch (var) {
+#define X(id, trav, lds, wpe) case id: return lds;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
+int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem) {
     switch (stack) {
-        case 16: return blocks_per_cu_s<16>(stats);
-        case 32: return blocks_per_cu_s<32>(stats);
-        default: return blocks_per_cu_s<64>(stats);
+        case 16: return stats ? occ_var<16, true>(var, smem) : occ_var<16, false>(var, smem);
+        case 32: return stats ? occ_var<32, true>(var, smem) : occ_var<32, false>(var, smem);
+        default: return stats ? occ_var<64, true>(var, smem) : occ_var<64, false>(var, smem);
     }
 }
 

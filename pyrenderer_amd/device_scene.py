@@ -87,3 +87,9 @@ class DeviceScene:
         s = np.zeros(4, np.uint64)
         N.check(N.lib().prt_last_stats(self.h, N.ptr(s)))
         return s
+
+    def diag_stats(self):
+        """16 diagnostic words of the last PRT_FLAG_STATS call (see include/prt.h)."""
+        s = np.zeros(16, np.uint64)
+        N.check(N.lib().prt_diag_stats(self.h, N.ptr(s)))
+        return s

@@ -1,0 +1,62 @@
+"""One process per GPU: interleaved tile sharding + RCCL gather.
+
+Every rank renders the 64x64 tiles with id % world == rank (load balance over
+the light-heavy and escape-heavy parts of the frame) into a device buffer of
+per-tile radiance sums; the buffers are gathered to rank 0 with
+torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" on CPU
+for tests) and rank 0 scatters the tiles into the (W, H, 3) frame.  Random
+numbers are keyed by (seed, global pixel, sample), so the frame is
+bit-identical for any world size.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .device_scene import interleaved_tiles, tile_grid, unpack_tiles
+
+
+class TileShard:
+    """This rank's tiles and the padded gather buffers (allocated once)."""
+
+    def __init__(self, W, H, tile, rank, world, device):
+        self.W, self.H, self.tile, self.rank, self.world = W, H, tile, rank, world
+        tx, ty = tile_grid(W, H, tile)
+        self.n_tiles = tx * ty
+        self.tiles = interleaved_tiles(W, H, tile, rank, world)
+        self.max_tiles = (self.n_tiles + world - 1) // world
+        self.slot_elems = tile * tile * 3
+        self.buf = torch.zeros(self.max_tiles * self.slot_elems, dtype=torch.float32, device=device)
+        self.gather_list = ([torch.empty_like(self.buf) for _ in range(world)]
+                            if (world > 1 and rank == 0) else None)
+
+    def gather(self, group=None):
+        """Collective: rank 0 receives every rank's tile sums (no-op for world 1)."""
+        if self.world > 1:
+            dist.gather(self.buf, self.gather_list, dst=0, group=group)
+
+    def assemble(self):
+        """Rank 0: (W, H, 3) float32 sums frame from the gathered buffers."""
+        frame = np.zeros((self.W, self.H, 3), np.float32)
+        bufs = self.gather_list if self.world > 1 else [self.buf]
+        for r, b in enumerate(bufs):
+            ids = interleaved_tiles(self.W, self.H, self.tile, r, self.world)
+            n = len(ids) * self.slot_elems
+            unpack_tiles(b[:n].cpu().numpy().reshape(-1, 3), self.W, self.H, self.tile, self.tile, ids, frame)
+        return frame
+
+
+def render_distributed(device_scene, cam_packed, W, H, spp, depth, seed=0, tile=64, group=None, stream=None):
+    """Render a frame across the ranks of the default group; returns mean radiance
+    (W, H, 3) on rank 0 and None elsewhere."""
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    dev = torch.device("cuda", device_scene.device)
+    shard = TileShard(W, H, tile, rank, world, dev)
+    s = stream or torch.cuda.current_stream(dev)
+    device_scene.render_tiles_device(cam_packed, W, H, tile, tile, shard.tiles, spp, depth, shard.buf.data_ptr(),
+                                     s.cuda_stream, seed=seed)
+    shard.gather(group)
+    if rank != 0:
+        return None
+    torch.cuda.synchronize(dev)
+    return shard.assemble() / np.float32(max(spp, 1))

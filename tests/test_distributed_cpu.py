@@ -1,0 +1,61 @@
+"""world_size-2 gloo run of the tile-shard + gather path on CPU (the oracle
+stands in for the GPU renderer): the gathered frame equals the single-process
+frame bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import CORNELL_JSON, ROOT
+
+W, H, TILE, SPP, DEPTH, SEED = 40, 36, 16, 2, 4, 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    from pyrenderer_amd.distributed import TileShard
+    from pyrenderer_amd.flatten import flatten_scene
+    from pyrenderer_amd.io_utils.read_tungsten import read_file
+    scene, cam = read_file(CORNELL_JSON)
+    osc = O.OracleScene.from_flat(flatten_scene(scene))
+    shard = TileShard(W, H, TILE, rank, world, torch.device("cpu"))
+    sums = osc.render_tiles(cam.convert_to_taichi_camera().packed(), W, H, TILE, TILE, shard.tiles, SPP, DEPTH,
+                            seed=SEED, nthreads=1)
+    shard.buf[:sums.size] = torch.from_numpy(sums.reshape(-1))
+    shard.gather()
+    if rank == 0:
+        np.save(out_path, shard.assemble())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_matches_single_process(tmp_path, world):
+    out = str(tmp_path / "frame.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    frame = np.load(out)
+    from oracle import oracle as O
+    from pyrenderer_amd.flatten import flatten_scene
+    from pyrenderer_amd.io_utils.read_tungsten import read_file
+    scene, cam = read_file(CORNELL_JSON)
+    ref = O.OracleScene.from_flat(flatten_scene(scene)).render(cam.convert_to_taichi_camera().packed(), W, H, SPP,
+                                                                DEPTH, seed=SEED, tile=TILE)
+    np.testing.assert_array_equal(frame, ref)
+    assert frame.sum() > 0

@@ -1,0 +1,77 @@
+"""A/B the trace-kernel variants on one device, interleaved rounds in one process
+(cdna_hip_programming.md §5.4 rule 24).  Checks every variant's image is
+bit-identical, prints per-variant median/min trace-kernel ms and Msamples/s.
+
+    python tools/ab_variants.py --res 512 --spp 64 --depth 8 --rounds 5 --variants 1 2 3
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", type=int, nargs="+", default=[1, 2, 3])
+    ap.add_argument("--scene", default="cornell", help="cornell | soup:N (random triangle soup of N tris in the box)")
+    a = ap.parse_args()
+    from pyrenderer_amd._native import PRT_FLAG_TIME
+    from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
+    from pyrenderer_amd.flatten import flatten_scene
+    from pyrenderer_amd.io_utils.read_tungsten import read_file
+    scene, cam = read_file(os.path.join(ROOT, "pyrenderer_amd", "media", "cornell-box", "scene.json"))
+    flat = flatten_scene(scene)
+    if a.scene.startswith("soup:"):
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from test_gpu_parity import _soup_scene
+        flat = _soup_scene((scene, cam, flat), int(a.scene.split(":")[1]), 9)
+    ds = DeviceScene(flat, 0)
+    c = cam.convert_to_taichi_camera().packed()
+    W = H = a.res
+    ids = interleaved_tiles(W, H, 64)
+    res = {v: [] for v in a.variants}
+    ref = None
+    for r in range(a.rounds + 1):
+        for v in a.variants:
+            flags = PRT_FLAG_TIME | (v << 8)
+            t0 = time.perf_counter()
+            out, _ = ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, flags)
+            wall = time.perf_counter() - t0
+            ms, n = ds.kernel_timing()
+            if ref is None:
+                ref = out
+            same = bool(np.array_equal(out, ref))
+            if r > 0:  # round 0 = warm-up
+                res[v].append((ms, wall * 1e3, same))
+    samples = W * H * a.spp
+    from pyrenderer_amd._native import PRT_FLAG_STATS
+    for v in a.variants:
+        ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, PRT_FLAG_STATS | (v << 8))
+        dg = ds.diag_stats().astype(np.float64)
+        tot = dg[4] + dg[5] + dg[6]
+        print(json.dumps({"variant": v, "diag": {"refill_frac": round(dg[4] / tot, 3), "trav_frac": round(dg[5] / tot, 3),
+                                                 "shade_frac": round(dg[6] / tot, 3), "wave_iters": int(dg[7]),
+                                                 "lanes_per_iter": round(dg[8] / max(dg[7], 1), 2),
+                                                 "nodes_per_sample": round(dg[0] / samples, 2),
+                                                 "tris_per_sample": round(dg[1] / samples, 2)}}), flush=True)
+    for v, rows in res.items():
+        ms = np.array([x[0] for x in rows])
+        print(json.dumps({"variant": v, "kernel_ms_median": round(float(np.median(ms)), 3),
+                          "kernel_ms_min": round(float(ms.min()), 3),
+                          "msamples_s": round(samples / np.median(ms) / 1e3, 1),
+                          "identical_to_first": all(x[2] for x in rows), "scene": a.scene,
+                          "bvh_depth": ds.bvh_depth, "nodes": ds.n_nodes}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
