@@ -142,7 +142,7 @@ __device__ __forceinline__ void gen_ray(const float* cam, float u, float v, uint
 }
 
 // ---------------------------------------------------------------- traversal
-struct Counters { uint32_t nodes, tris, ext, shadow; };
+struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf; };
 
 // Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
 __device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 o, V3 inv,
@@ -339,7 +339,7 @@ __device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, co
         while (cur >= 0 && cur != kSentinel) {
             const float4* nd = nodes + (size_t)cur * 4;
             float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            if (STATS) cn.nodes++;
+            if (STATS) { cn.nodes++; cn.it_inner++; }
             float tl, tr;
             bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, best, tl);
             bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tmin, best, tr);
@@ -366,6 +366,7 @@ __device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, co
         while (leaf < 0) {
             int v = -leaf - 1;
             int first = v >> 3, cnt = (v & 7) + 1;
+            if (STATS) cn.it_leaf++;
             for (int k = 0; k < cnt; ++k) {
                 const float4* tp = tris + (size_t)(first + k) * 3;
                 float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
@@ -397,12 +398,13 @@ template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel(TraceParams P) {
     extern __shared__ float4 smem[];
+    constexpr int kStackWords = STACK;
     int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
     const float4* g_nodes = P.nodes;
     const float4* g_tris = P.tris;
     if (SCENE_LDS) {
         // small scene: copy BVH + triangles into LDS once per persistent block
-        float4* sn = smem + STACK * kBlock / 4;
+        float4* sn = smem + kStackWords * kBlock / 4;
         float4* st4 = sn + P.n_node_f4;
         for (int i = threadIdx.x; i < P.n_node_f4; i += kBlock) sn[i] = P.nodes[i];
         for (int i = threadIdx.x; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
@@ -424,7 +426,8 @@ void trace_kernel(TraceParams P) {
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
     V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
     float tmax = kTMax;
-    Counters cn = {0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0};
+    uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
     const uint32_t tile_px = (uint32_t)(P.tw * P.th);
 
     // diagnostic (STATS) wave-level clocks: refill / traversal / shading, iterations, active lanes
@@ -514,6 +517,14 @@ void trace_kernel(TraceParams P) {
             t_b = __builtin_amdgcn_s_memtime();
             c_trav += t_b - t_a;
             t_a = t_b;
+            // wave-level loop trips = max over lanes; lane-level = sum
+            uint32_t mi = cn.it_inner, ml = cn.it_leaf;
+            for (int off = 32; off > 0; off >>= 1) {
+                mi = max(mi, (uint32_t)__shfl_xor((int)mi, off));
+                ml = max(ml, (uint32_t)__shfl_xor((int)ml, off));
+            }
+            w_inner += mi; w_leaf += ml; l_inner += cn.it_inner; l_leaf += cn.it_leaf;
+            cn.it_inner = 0; cn.it_leaf = 0;
         }
         // ------------------------------------------------- shade the result
         bool finished = false;
@@ -615,6 +626,16 @@ void trace_kernel(TraceParams P) {
             atomicAdd(P.stats + 6, (unsigned long long)c_shade);
             atomicAdd(P.stats + 7, (unsigned long long)n_iter);
             atomicAdd(P.stats + 8, (unsigned long long)n_active);
+            atomicAdd(P.stats + 9, (unsigned long long)w_inner);
+            atomicAdd(P.stats + 10, (unsigned long long)w_leaf);
+        }
+        {
+            uint64_t a2 = l_inner, b2 = l_leaf;
+            for (int off = 32; off > 0; off >>= 1) { a2 += __shfl_down(a2, off); b2 += __shfl_down(b2, off); }
+            if (lane == 0) {
+                atomicAdd(P.stats + 11, (unsigned long long)a2);
+                atomicAdd(P.stats + 12, (unsigned long long)b2);
+            }
         }
     }
 }
@@ -667,7 +688,7 @@ static hipError_t launch_stack(const TraceParams& P, int var, int grid, bool sta
 bool variant_uses_lds(int var);
 
 // entries needed: one per level (<= depth) plus the while-while sentinel
-int stack_variant(int depth) { return depth + 1 <= 16 ? 16 : depth + 1 <= 32 ? 32 : 64; }
+int stack_variant(int depth) { return depth + 1 <= 10 ? 10 : depth + 1 <= 16 ? 16 : depth + 1 <= 32 ? 32 : 64; }
 
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
     size_t b = (size_t)stack * kBlock * sizeof(int);
@@ -678,6 +699,7 @@ size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream) {
     size_t smem = trace_smem_bytes(stack, var, P);
     switch (stack) {
+        case 10: return launch_stack<10>(P, var, grid, stats, smem, stream);
         case 16: return launch_stack<16>(P, var, grid, stats, smem, stream);
         case 32: return launch_stack<32>(P, var, grid, stats, smem, stream);
         default: return launch_stack<64>(P, var, grid, stats, smem, stream);
@@ -714,6 +736,7 @@ bool variant_uses_lds(int var) {
 
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem) {
     switch (stack) {
+        case 10: return stats ? occ_var<10, true>(var, smem) : occ_var<10, false>(var, smem);
         case 16: return stats ? occ_var<16, true>(var, smem) : occ_var<16, false>(var, smem);
         case 32: return stats ? occ_var<32, true>(var, smem) : occ_var<32, false>(var, smem);
         default: return stats ? occ_var<64, true>(var, smem) : occ_var<64, false>(var, smem);

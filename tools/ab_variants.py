@@ -63,7 +63,12 @@ def main():
                                                  "shade_frac": round(dg[6] / tot, 3), "wave_iters": int(dg[7]),
                                                  "lanes_per_iter": round(dg[8] / max(dg[7], 1), 2),
                                                  "nodes_per_sample": round(dg[0] / samples, 2),
-                                                 "tris_per_sample": round(dg[1] / samples, 2)}}), flush=True)
+                                                 "tris_per_sample": round(dg[1] / samples, 2),
+                                                 "inner_simd_eff": round(dg[11] / max(dg[9] * 64, 1), 3),
+                                                 "leaf_simd_eff": round(dg[12] / max(dg[10] * 64, 1), 3),
+                                                 "wave_inner_trips_per_iter": round(dg[9] / max(dg[7], 1), 2),
+                                                 "wave_leaf_trips_per_iter": round(dg[10] / max(dg[7], 1), 2)}}),
+              flush=True)
     for v, rows in res.items():
         ms = np.array([x[0] for x in rows])
         print(json.dumps({"variant": v, "kernel_ms_median": round(float(np.median(ms)), 3),
