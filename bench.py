@@ -38,28 +38,65 @@ B_NODE, B_TRI, B_LIGHT, B_SAMPLE, B_PIXEL = 64, 48, 64, 24, 12
 F_NODE, F_TRI = 40, 45
 
 
+# BASELINE.json configs; the bench line is quoted on config 2.
+CONFIGS = {
+    1: dict(scene="cornell", res=128, spp=4, depth=4),
+    2: dict(scene="cornell", res=512, spp=64, depth=8),
+    3: dict(scene="specular", res=1024, spp=256, depth=8),
+    4: dict(scene="cubes", res=512, spp=64, depth=8),
+    5: dict(scene="cornell", res=4096, spp=256, depth=8),
+}
+
+
+SCENE_NAMES = {"cornell": "Cornell box (Lambertian)", "specular": "Cornell box + metal/dielectric + sphere",
+               "cubes": "Cornell box + 1M-triangle instanced cube.obj"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--res", type=int, default=512)
-    ap.add_argument("--spp", type=int, default=64)
-    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--scene", default=None, help="cornell | specular | cubes (overrides --config)")
+    ap.add_argument("--res", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per trace launch (tools/pmc_traffic.py); null if absent")
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in CONFIGS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
+
+
+def load_scene(name):
+    from pyrenderer_amd import scenes
+    from pyrenderer_amd.io_utils.read_tungsten import read_file
+    if name == "cornell":
+        return read_file(scenes.CORNELL)
+    if name == "specular":
+        return read_file(scenes.CORNELL_SPECULAR)
+    if name == "cubes":
+        return scenes.instanced_cubes()
+    raise SystemExit(f"unknown scene {name}")
 
 
 def cpu_baseline(flat, cam, args):
     """Oracle (C restatement of PathTracer.trace, OpenMP) on a bounded sample of the
-    same workload: a subset of 8x8 tiles at the full spp/depth."""
+    same workload: a subset of 8x8 tiles at the full spp/depth.  Closest hits by
+    stack traversal of the same BVH2 (oracle BACKEND_BVH, bit-identical to the
+    brute-force and reference-structure backends and the fastest of the three)."""
     from oracle import oracle as O
+    from pyrenderer_amd._native import Bvh
     osc = O.OracleScene.from_flat(flat)
+    nodes, _, order = Bvh(flat.tri_v).export()
+    osc.set_bvh(nodes, order)
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
     W = H = args.res
     n_tiles_total = (W // 8) * (H // 8)
@@ -67,18 +104,20 @@ def cpu_baseline(flat, cam, args):
     perm = rng.permutation(n_tiles_total).astype(np.int32)
     # calibrate on 4 tiles, then size the sample for ~args.cpu_seconds
     t0 = time.perf_counter()
-    osc.render_tiles(cam, W, H, 8, 8, perm[:4], args.spp, args.depth, seed=args.seed, nthreads=cores)
+    osc.render_tiles(cam, W, H, 8, 8, perm[:4], args.spp, args.depth, seed=args.seed, nthreads=cores,
+                     backend=O.BACKEND_BVH)
     dt = max(time.perf_counter() - t0, 1e-3)
     n = int(min(n_tiles_total, max(8, 4 * args.cpu_seconds / dt)))
     ids = np.sort(perm[:n])
     t0 = time.perf_counter()
-    osc.render_tiles(cam, W, H, 8, 8, ids, args.spp, args.depth, seed=args.seed, nthreads=cores)
+    osc.render_tiles(cam, W, H, 8, 8, ids, args.spp, args.depth, seed=args.seed, nthreads=cores,
+                     backend=O.BACKEND_BVH)
     dt = time.perf_counter() - t0
     samples = n * 64 * args.spp
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
             "sample": f"{n} random 8x8 tiles of the {W}x{H} frame at {args.spp} spp, depth {args.depth} "
-                      f"({samples} samples, {dt:.1f} s); oracle/prt_oracle.c, reference-structure-free brute-force "
-                      f"closest hit, OpenMP"}
+                      f"({samples} samples, {dt:.1f} s); oracle/prt_oracle.c (C port of PathTracer.trace), "
+                      f"BVH2 closest hit, OpenMP {cores} threads"}
 
 
 def main():
@@ -101,9 +140,8 @@ def main():
     from pyrenderer_amd.device_scene import DeviceScene
     from pyrenderer_amd.distributed import TileShard
     from pyrenderer_amd.flatten import flatten_scene
-    from pyrenderer_amd.io_utils.read_tungsten import read_file
 
-    scene, camera = read_file(os.path.join(ROOT, "pyrenderer_amd", "media", "cornell-box", "scene.json"))
+    scene, camera = load_scene(args.scene)
     flat = flatten_scene(scene)
     cam = camera.convert_to_taichi_camera().packed()
     t_build = time.perf_counter()
@@ -163,19 +201,20 @@ def main():
         if tj and os.path.exists(tj):
             try:
                 d = json.load(open(tj))
-                if d.get("config") == f"{W}x{H}x{args.spp}spp_d{args.depth}" and world == 1:
+                if d.get("config") == f"{args.scene}_{W}x{H}x{args.spp}spp_d{args.depth}" and world == 1:
                     traffic = d.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and rank == 0:
             cpu = cpu_baseline(flat, cam, args)
         line = {
             "metric": "Msamples/sec Cornell box 512²×64spp at 1/2/4/8 GPU; per-pixel L2 vs CPU",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic (Cornell box scene.json)",
-            "config": {"workload": f"Cornell box {W}x{H}, {args.spp} spp, depth {args.depth}, Lambertian",
+            "config": {"workload": f"{SCENE_NAMES[args.scene]} {W}x{H}, {args.spp} spp, depth {args.depth}",
+                       "baseline_config": args.config, "triangles": int(flat.n_tri), "spheres": int(flat.sph.shape[0]),
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
                        "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -22,6 +22,7 @@ _LIB_PATH = os.path.join(_HERE, "_build", "libprt_oracle.so")
 
 BACKEND_REF = 0     # reference structure: median-split BVH over primitives + per-primitive loop
 BACKEND_BRUTE = 1   # all triangles, closest (t, index)
+BACKEND_BVH = 2     # stack traversal of an external BVH2 (prt_bvh_export arrays); boxes only prune
 
 _f = ctypes.c_float
 _i = ctypes.c_int
@@ -47,9 +48,11 @@ def lib():
             build()
         L = ctypes.CDLL(_LIB_PATH)
         L.or_scene_create.restype = _vp
-        L.or_scene_create.argtypes = [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _i32, _vp, _vp, _i32, _vp]
+        L.or_scene_create.argtypes = [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _i32, _vp, _vp, _i64, _vp, _i32, _vp, _vp,
+                                      _i32, _vp]
         L.or_scene_destroy.argtypes = [_vp]
         L.or_set_trig_mode.argtypes = [_i]
+        L.or_scene_set_bvh.argtypes = [_vp, _vp, _i64, _vp]
         L.or_ref_bvh.argtypes = [_vp] + [_vp] * 6
         L.or_mt.argtypes = [_vp] * 5 + [_f, _f, _vp]
         L.or_aabb.argtypes = [_vp] * 4 + [_f, _f]
@@ -94,29 +97,40 @@ class OracleScene:
     face lists; direct_rgb the directly-hit light colour (core/tracing.py:120).
     """
 
-    def __init__(self, tri_v, tri_n, tri_mat, tri_prim, prim_lo, prim_hi, mat, light_tri, light_off, direct_rgb):
+    def __init__(self, tri_v, tri_n, tri_mat, tri_prim, prim_lo, prim_hi, mat, light_tri, light_off, direct_rgb,
+                 sph=None, sph_mat=None):
+        sph = np.zeros((0, 4), np.float32) if sph is None else sph
+        sph_mat = np.zeros(0, np.int32) if sph_mat is None else sph_mat
         self._keep = [_f32(tri_v, (-1, 9)), _f32(tri_n, (-1, 3)), np.ascontiguousarray(tri_mat, np.int32),
                       np.ascontiguousarray(tri_prim, np.int32), _f32(prim_lo, (-1, 3)), _f32(prim_hi, (-1, 3)),
                       _f32(mat, (-1, 8)), np.ascontiguousarray(light_tri, np.int32),
-                      np.ascontiguousarray(light_off, np.int32), _f32(direct_rgb, (3,))]
+                      np.ascontiguousarray(light_off, np.int32), _f32(direct_rgb, (3,)),
+                      _f32(sph, (-1, 4)), np.ascontiguousarray(sph_mat, np.int32)]
         k = self._keep
         self.n_tri = k[0].shape[0]
         self.n_prim = k[4].shape[0]
         self.h = lib().or_scene_create(_p(k[0]), _p(k[1]), _p(k[2]), _p(k[3]), self.n_tri, _p(k[4]), _p(k[5]),
-                                       self.n_prim, _p(k[6]), k[6].shape[0], _p(k[7]), _p(k[8]),
-                                       k[8].shape[0] - 1, _p(k[9]))
+                                       self.n_prim, _p(k[10]), _p(k[11]), k[10].shape[0], _p(k[6]), k[6].shape[0],
+                                       _p(k[7]), _p(k[8]), k[8].shape[0] - 1, _p(k[9]))
 
     @classmethod
     def from_flat(cls, flat):
         """Build from a pyrenderer_amd FlatScene-like object or dict."""
         g = flat if isinstance(flat, dict) else flat.__dict__
         return cls(g["tri_v"], g["tri_n"], g["tri_mat"], g["tri_prim"], g["prim_lo"], g["prim_hi"], g["mat"],
-                   g["light_tri"], g["light_off"], g["direct_rgb"])
+                   g["light_tri"], g["light_off"], g["direct_rgb"], g.get("sph"), g.get("sph_mat"))
 
     def __del__(self):
         if getattr(self, "h", None):
             lib().or_scene_destroy(self.h)
             self.h = None
+
+    def set_bvh(self, nodes, order):
+        """Attach BVH2 arrays (from pyrenderer_amd's prt_bvh_export) for BACKEND_BVH."""
+        nodes = _f32(nodes, (-1, 16))
+        order = np.ascontiguousarray(order, np.int32)
+        self._keep += [nodes, order]
+        lib().or_scene_set_bvh(self.h, _p(nodes), nodes.shape[0], _p(order))
 
     def ref_bvh(self):
         n = 2 * self.n_prim

@@ -285,6 +285,41 @@ static inline v3 refract3(v3 v, v3 n, float eta) {
     return add(perp, par);
 }
 
+/* random_in_unit_sphere (vec3_taichi.py:299-306): theta = 2 pi u1,
+ * cos(phi) = 2 u2 - 1, r = u3^(1/3).  Restated with deterministic f32 ops
+ * (quadrant reduction + the minimax polynomials, Newton cube root) so CPU
+ * and GPU draw identical points; acos is not needed (sin(phi) = sqrt(1-z^2)). */
+static inline float cbrt_spec(float x) {
+    if (!(x > 0.0f)) return 0.0f;
+    union { float f; uint32_t u; } b;
+    b.f = x;
+    b.u = b.u / 3u + 709921077u;
+    float y = b.f;
+    for (int i = 0; i < 3; ++i) y = (2.0f * y + x / (y * y)) / 3.0f;
+    return y;
+}
+static inline void sincos_2pi(float u, float* c, float* sn) {
+    int q = (int)floorf(u * 4.0f + 0.5f);
+    float a = 6.28318530717958647692f * (u - 0.25f * (float)q);   /* in [-pi/4, pi/4] */
+    float pc = poly_cos(a), ps = poly_sin(a);
+    switch (q & 3) {
+        case 0: *c = pc; *sn = ps; break;
+        case 1: *c = -ps; *sn = pc; break;
+        case 2: *c = -pc; *sn = -ps; break;
+        default: *c = ps; *sn = -pc; break;
+    }
+}
+static inline v3 random_in_unit_sphere(Rng* rng) {
+    float u1 = rng_next(rng), u2 = rng_next(rng), u3 = rng_next(rng);
+    float c, sn;
+    sincos_2pi(u1, &c, &sn);
+    float z = 2.0f * u2 - 1.0f;
+    float m = 1.0f - z * z;
+    float sp = sqrtf(m > 0.0f ? m : 0.0f);
+    float r = cbrt_spec(u3);
+    return mk(r * sp * c, r * sp * sn, r * z);
+}
+
 /* ------------------------------------------------------------------ scene */
 typedef struct {
     /* triangles (original order) */
@@ -297,11 +332,19 @@ typedef struct {
     /* materials: rho.rgb, emit, sided, type, ior, roughness */
     int32_t n_mat;
     float* mat;
+    /* spheres (build-added primitive; hit = intersection_taichi.py:15-36) */
+    int64_t n_sph;
+    float* sph;                        /* n_sph x 4: center, radius */
+    int32_t* sph_mat;
     /* lights */
     int32_t n_light;
     int32_t* light_tri;
     int32_t* light_off;
     float direct_rgb[3];
+    /* optional external BVH2 (prt_bvh_export layout) for the BACKEND_BVH traversal */
+    int64_t x_nodes;
+    float* xnode;                      /* x_nodes x 16 */
+    int32_t* xorder;                   /* BVH slot -> triangle */
     /* reference-structure BVH over primitives (bvh_taichi.py) */
     int32_t n_prim;
     int32_t* prim_first; int32_t* prim_count;
@@ -340,10 +383,18 @@ OR_API void or_set_trig_mode(int m) { g_trig_mode = m; }
 OR_API void* or_scene_create(const float* tri_v, const float* tri_n, const int32_t* tri_mat,
                              const int32_t* tri_prim, int64_t n_tri,
                              const float* prim_lo, const float* prim_hi, int32_t n_prim,
+                             const float* sph, const int32_t* sph_mat, int64_t n_sph,
                              const float* mat, int32_t n_mat,
                              const int32_t* light_tri, const int32_t* light_off, int32_t n_light,
                              const float* direct_rgb) {
     OScene* s = (OScene*)calloc(1, sizeof(OScene));
+    s->n_sph = n_sph;
+    s->sph = (float*)malloc(sizeof(float) * 4 * (n_sph > 0 ? n_sph : 1));
+    s->sph_mat = (int32_t*)malloc(sizeof(int32_t) * (n_sph > 0 ? n_sph : 1));
+    if (n_sph > 0) {
+        memcpy(s->sph, sph, sizeof(float) * 4 * n_sph);
+        memcpy(s->sph_mat, sph_mat, sizeof(int32_t) * n_sph);
+    }
     s->n_tri = n_tri;
     s->v0 = (float*)malloc(sizeof(float) * 3 * n_tri);
     s->e1 = (float*)malloc(sizeof(float) * 3 * n_tri);
@@ -420,7 +471,8 @@ OR_API void or_scene_destroy(void* p) {
     OScene* s = (OScene*)p;
     if (!s) return;
     free(s->v0); free(s->e1); free(s->e2); free(s->vtx); free(s->nrm); free(s->mat_id); free(s->prim_id);
-    free(s->mat); free(s->light_tri); free(s->light_off);
+    free(s->mat); free(s->light_tri); free(s->light_off); free(s->sph); free(s->sph_mat);
+    free(s->xnode); free(s->xorder);
     free(s->prim_first); free(s->prim_count);
     free(s->bobj); free(s->bleft); free(s->bright); free(s->bnext); free(s->bmin); free(s->bmax);
     free(s);
@@ -439,6 +491,18 @@ static inline v3 tri_v0(const OScene* s, int64_t i) { return ld3(s->v0 + 3 * i);
 static inline v3 tri_e1(const OScene* s, int64_t i) { return ld3(s->e1 + 3 * i); }
 static inline v3 tri_e2(const OScene* s, int64_t i) { return ld3(s->e2 + 3 * i); }
 static inline const float* matp(const OScene* s, int64_t tri) { return s->mat + 8 * s->mat_id[tri]; }
+
+/* Hit id space: [0, n_tri) triangles, [n_tri, n_tri + n_sph) spheres. */
+static inline const float* mat_of(const OScene* s, int64_t id) {
+    if (id < s->n_tri) return s->mat + 8 * s->mat_id[id];
+    return s->mat + 8 * s->sph_mat[id - s->n_tri];
+}
+/* geometric (unflipped) normal: stored face normal, or (p - c) / r for spheres */
+static inline v3 geo_normal(const OScene* s, int64_t id, v3 p) {
+    if (id < s->n_tri) return ld3(s->nrm + 3 * id);
+    const float* c = s->sph + 4 * (id - s->n_tri);
+    return mk((p.x - c[0]) / c[3], (p.y - c[1]) / c[3], (p.z - c[2]) / c[3]);
+}
 
 /* Shading frame + scatter of Quad.hit/Cube.hit (shapes.py:98-108): flip the
  * face normal toward the ray for two-sided BSDFs, draw the cosine-hemisphere
@@ -515,20 +579,103 @@ static Hit hit_all_brute(const OScene* s, v3 ro, v3 rd, float t_min, float t_max
         }
     }
     if (cnt) cnt[1] += (uint64_t)s->n_tri;
+    if (!(any_hit && h.hit)) {
+        for (int64_t k = 0; k < s->n_sph; ++k) {
+            float root;
+            const float* c = s->sph + 4 * k;
+            if (sphere_hit(mk(c[0], c[1], c[2]), c[3], ro, rd, t_min, best, &root)) {
+                best = root; h.hit = 1; h.tri = s->n_tri + k;
+                if (any_hit) break;
+            }
+        }
+    }
     h.t = best;
-    if (h.hit) h.n = shade_normal(s, h.tri, rd);
     return h;
 }
 
-enum { BACKEND_REF = 0, BACKEND_BRUTE = 1 };
+/* Traversal of an external BVH2 (nodes from prt_bvh_export: two child boxes +
+ * refs per 64-B node; leaf ref < 0 encodes (first slot, count)).  Boxes only
+ * prune, so the result is the brute-force closest (t, index) hit; the slab test
+ * is the reference's (bvh_taichi.py:168-190) with t1 = closest so far. */
+static Hit hit_all_bvh(const OScene* s, v3 ro, v3 rd, float t_min, float t_max, int any_hit, uint64_t* cnt) {
+    Hit h; memset(&h, 0, sizeof(h));
+    float best = t_max;
+    int64_t best_id = -1;
+    int32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        int32_t cur = stack[--sp];
+        if (cur >= 0) {
+            const float* nd = s->xnode + 16 * (int64_t)cur;
+            if (cnt) cnt[0]++;
+            for (int side = 1; side >= 0; --side) {
+                const float* b = nd + 6 * side;
+                float lo[3] = {b[0], b[2], b[4]}, hi[3] = {b[1], b[3], b[5]};
+                if (aabb_hit(lo, hi, ro, rd, t_min, best)) {
+                    int32_t ref;
+                    memcpy(&ref, nd + 12 + side, 4);
+                    if (sp < 128) stack[sp++] = ref;
+                }
+            }
+        } else {
+            int32_t v = -cur - 1;
+            int64_t first = v >> 3, count = (v & 7) + 1;
+            for (int64_t k = first; k < first + count; ++k) {
+                int64_t i = s->xorder[k];
+                float t;
+                if (cnt) cnt[1]++;
+                if (mt_hit(tri_v0(s, i), tri_e1(s, i), tri_e2(s, i), ro, rd, t_min, t_max, &t) &&
+                    (t < best || (t == best && best_id >= 0 && i < best_id))) {
+                    best = t; best_id = i;
+                    if (any_hit) { sp = 0; break; }
+                }
+            }
+        }
+    }
+    h.hit = best_id >= 0;
+    h.tri = best_id;
+    if (!(any_hit && h.hit)) {
+        for (int64_t k = 0; k < s->n_sph; ++k) {
+            float root;
+            const float* c = s->sph + 4 * k;
+            if (sphere_hit(mk(c[0], c[1], c[2]), c[3], ro, rd, t_min, best, &root)) {
+                best = root; h.hit = 1; h.tri = s->n_tri + k;
+                if (any_hit) break;
+            }
+        }
+    }
+    h.t = best;
+    return h;
+}
+
+OR_API int or_scene_set_bvh(void* p, const float* nodes, int64_t n_nodes, const int32_t* order) {
+    OScene* s = (OScene*)p;
+    free(s->xnode); free(s->xorder);
+    s->x_nodes = n_nodes;
+    s->xnode = (float*)malloc(sizeof(float) * 16 * n_nodes);
+    s->xorder = (int32_t*)malloc(sizeof(int32_t) * (s->n_tri > 0 ? s->n_tri : 1));
+    memcpy(s->xnode, nodes, sizeof(float) * 16 * n_nodes);
+    memcpy(s->xorder, order, sizeof(int32_t) * s->n_tri);
+    return 0;
+}
+
+enum { BACKEND_REF = 0, BACKEND_BRUTE = 1, BACKEND_BVH = 2 };
 
 static Hit closest_hit(const OScene* s, int backend, v3 ro, v3 rd, float t0, float t1, uint64_t* cnt) {
     if (backend == BACKEND_REF) return hit_all_ref(s, ro, rd, t0, t1, NULL, 0, cnt);
-    return hit_all_brute(s, ro, rd, t0, t1, 0, cnt);
+    Hit h = backend == BACKEND_BVH ? hit_all_bvh(s, ro, rd, t0, t1, 0, cnt) : hit_all_brute(s, ro, rd, t0, t1, 0, cnt);
+    if (h.hit) {
+        v3 ng = geo_normal(s, h.tri, add(ro, scl(rd, h.t)));
+        const float* m = mat_of(s, h.tri);
+        h.n = (m[4] == 0.0f && dot(ng, neg(rd)) < 0.0f) ? neg(ng) : ng;
+    }
+    return h;
 }
 
 static int occluded(const OScene* s, int backend, v3 ro, v3 rd, float t0, float t1, uint64_t* cnt) {
     if (backend == BACKEND_REF) return hit_all_ref(s, ro, rd, t0, t1, NULL, 0, cnt).hit;
+    if (backend == BACKEND_BVH) return hit_all_bvh(s, ro, rd, t0, t1, 1, cnt).hit;
     return hit_all_brute(s, ro, rd, t0, t1, 1, cnt).hit;
 }
 
@@ -570,7 +717,7 @@ static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, in
         if (scripted) h = hit_all_ref(s, ro, rd, kTMin, kTMax, rng, 1, cnt);
         else h = closest_hit(s, backend, ro, rd, kTMin, kTMax, cnt);
         if (!h.hit) break;
-        const float* m = matp(s, h.tri);
+        const float* m = mat_of(s, h.tri);
         v3 n = h.n;
         if (m[3] != 0.0f) {  /* emitter: tracing.py:129-139 */
             float d1 = dot(neg(rd), n);
@@ -579,6 +726,32 @@ static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, in
                 else L = add(L, scl(mul(lc, beta), d1));
             }
             break;
+        }
+        if (m[5] == 2.0f || m[5] == 3.0f) {
+            /* specular BSDFs (build-added, config 3): bsdf_taichi.py:52-59 / :69-86.
+             * Delta distributions: beta *= albedo, no NEE, next ray = the scattered one. */
+            v3 p = add(ro, scl(rd, h.t));
+            v3 ng = geo_normal(s, h.tri, p);
+            int front = dot(rd, ng) < 0.0f;
+            v3 ns = front ? ng : neg(ng);
+            v3 unit = normalize(rd);
+            v3 out;
+            if (m[5] == 2.0f) {
+                out = reflect3(unit, ns);
+                if (m[7] > 0.0f) out = add(out, scl(random_in_unit_sphere(rng), m[7]));
+                if (!(dot(out, ns) > 0.0f)) break;   /* absorbed */
+            } else {
+                float ratio = front ? 1.0f / m[6] : m[6];
+                float ct = -dot(unit, ns);
+                if (ct > 1.0f) ct = 1.0f;
+                float st = sqrtf(1.0f - ct * ct);
+                int cannot = ratio * st > 1.0f;
+                if (cannot || schlick(ct, ratio) > rng_next(rng)) out = reflect3(unit, ns);
+                else out = refract3(unit, ns, ratio);
+            }
+            beta = mul(beta, mk(m[0], m[1], m[2]));
+            ro = p; rd = normalize(out);
+            continue;
         }
         v3 wi; float pdf;
         if (scripted) { wi = h.wi; pdf = h.pdf; }

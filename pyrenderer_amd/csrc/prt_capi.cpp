@@ -65,12 +65,13 @@ struct Scene {
     int occ[32] = {0};               // blocks/CU per (variant, stats) once queried
     int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
-    DevBuf nodes, tris, tri_nm, mats, light_v, light_off;
+    DevBuf nodes, tris, tri_nm, mats, light_v, light_off, sph, sph_mat;
+    int64_t n_sph = 0;
     DevBuf tiles, buf, acc, work, stats;
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;   // start/stop pairs of the last timed call
     int ev_used = 0;
-    size_t chunk_bytes = (size_t)1 << 30;  // per-sample buffer budget
+    size_t chunk_bytes = (size_t)4 << 30;  // per-sample buffer budget (HBM is 288 GB)
     size_t device_bytes = 0;
 };
 
@@ -90,8 +91,8 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->nodes, &s->tris, &s->tri_nm, &s->mats, &s->light_v, &s->light_off, &s->tiles, &s->buf,
-                      &s->acc, &s->work, &s->stats})
+    for (DevBuf* b : {&s->nodes, &s->tris, &s->tri_nm, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
+                      &s->tiles, &s->buf, &s->acc, &s->work, &s->stats})
         b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -160,6 +161,10 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.stats = (unsigned long long*)s->stats.p;
     P.n_node_f4 = (int)s->n_node_f4;
     P.n_tri_f4 = (int)s->n_tri_f4;
+    P.n_tri = (int)s->n_tri;
+    P.n_sph = (int)s->n_sph;
+    P.sph = (const float4*)s->sph.p;
+    P.sph_mat = (const int*)s->sph_mat.p;
     int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFu);
     if (var == 0) var = default_variant(s);
     if (var < prt::kVarSplit || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
@@ -249,11 +254,15 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
                      const float* sph, const int32_t* sph_mat, int64_t n_sph, const float* mat, int32_t n_mat,
                      const int32_t* light_tri, const int32_t* light_off, int32_t n_light, const float* direct_rgb,
                      void** out_scene) {
-    (void)sph; (void)sph_mat;
     if (!out_scene) return fail(PRT_ERR_ARG, "out_scene is NULL");
     *out_scene = nullptr;
     if (n_tri < 0 || (n_tri > 0 && (!tri_v || !tri_n || !tri_mat))) return fail(PRT_ERR_ARG, "bad triangle arrays");
-    if (n_sph > 0) return fail(PRT_ERR_UNSUP, "spheres are not supported by this build yet");
+    if (n_sph < 0 || (n_sph > 0 && (!sph || !sph_mat))) return fail(PRT_ERR_ARG, "bad sphere arrays");
+    for (int64_t k = 0; k < n_sph; ++k) {
+        if (sph_mat[k] < 0 || sph_mat[k] >= n_mat) return fail(PRT_ERR_ARG, "sphere material id out of range");
+        if (!(sph[4 * k + 3] > 0.0f)) return fail(PRT_ERR_ARG, "sphere radius must be > 0");
+    }
+    if (n_tri + n_sph >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many primitives");
     if (n_mat < 1 || !mat) return fail(PRT_ERR_ARG, "need at least one material");
     if (n_light < 1 || !light_off || !light_tri) return fail(PRT_ERR_ARG, "There is no lights!!! (n_light < 1)");
     for (int64_t i = 0; i < n_tri; ++i)
@@ -314,6 +323,9 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         if ((rc = upload(s->mats, mat, sizeof(float) * 8 * (size_t)n_mat, &s->device_bytes))) break;
         if ((rc = upload(s->light_v, lv.data(), sizeof(float) * lv.size(), &s->device_bytes))) break;
         if ((rc = upload(s->light_off, light_off, sizeof(int32_t) * (size_t)(n_light + 1), &s->device_bytes))) break;
+        s->n_sph = n_sph;
+        if ((rc = upload(s->sph, sph, sizeof(float) * 4 * (size_t)n_sph, &s->device_bytes))) break;
+        if ((rc = upload(s->sph_mat, sph_mat, sizeof(int32_t) * (size_t)n_sph, &s->device_bytes))) break;
         if ((e = s->work.ensure(64)) != hipSuccess || (e = s->stats.ensure(8 * kStatWords)) != hipSuccess) {
             rc = fail(PRT_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
             break;

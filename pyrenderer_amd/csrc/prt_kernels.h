@@ -28,6 +28,10 @@ struct TraceParams {
     float* out;               // n_items x 3 radiance, item = (s - s0) * n_slots + slot
     unsigned long long* stats;  // 4 counters (nodes, tris, ext queries, shadow queries)
     int n_node_f4, n_tri_f4;  // scene sizes in float4 (LDS-resident variant)
+    int n_tri;                // hit ids >= n_tri are spheres
+    int n_sph;
+    const float4* sph;        // center xyz, radius
+    const int* sph_mat;
 };
 
 // trace kernel variants (A/B-able at run time through PRT_FLAG_VARIANT)

@@ -141,6 +141,63 @@ __device__ __forceinline__ void gen_ray(const float* cam, float u, float v, uint
     d = v3(f0 / l, f1 / l, f2 / l);
 }
 
+// -------------------------------------- specular helpers (bsdf_taichi.py:6-22)
+__device__ __forceinline__ float schlick(float cosine, float idx) {
+    float r0 = (1.0f - idx) / (1.0f + idx);
+    r0 = r0 * r0;
+    float m = 1.0f - cosine;
+    return r0 + (1.0f - r0) * (m * m * m * m * m);
+}
+__device__ __forceinline__ V3 reflect3(V3 v, V3 n) { return v - n * (2.0f * dot(v, n)); }
+__device__ __forceinline__ V3 refract3(V3 v, V3 n, float eta) {
+    float ct = -dot(v, n);
+    ct = ct > 1.0f ? 1.0f : ct;
+    V3 perp = (v + n * ct) * eta;
+    float k = 1.0f - dot(perp, perp);
+    return perp + n * (-sqrtf(fabsf(k)));
+}
+// random_in_unit_sphere (vec3_taichi.py:299-306) with deterministic ops: see oracle
+__device__ __forceinline__ float cbrt_spec(float x) {
+    if (!(x > 0.0f)) return 0.0f;
+    float y = __uint_as_float(__float_as_uint(x) / 3u + 709921077u);
+    for (int i = 0; i < 3; ++i) y = (2.0f * y + x / (y * y)) / 3.0f;
+    return y;
+}
+__device__ __forceinline__ V3 random_in_unit_sphere(uint32_t& st) {
+    float u1 = rng_next(st), u2 = rng_next(st), u3 = rng_next(st);
+    int q = (int)floorf(u1 * 4.0f + 0.5f);
+    float a = 6.28318530717958647692f * (u1 - 0.25f * (float)q);
+    float pc = poly_cos(a), ps = poly_sin(a);
+    float c, sn;
+    switch (q & 3) {
+        case 0: c = pc; sn = ps; break;
+        case 1: c = -ps; sn = pc; break;
+        case 2: c = -pc; sn = -ps; break;
+        default: c = ps; sn = -pc; break;
+    }
+    float z = 2.0f * u2 - 1.0f;
+    float m = 1.0f - z * z;
+    float sp = sqrtf(m > 0.0f ? m : 0.0f);
+    float r = cbrt_spec(u3);
+    return v3(r * sp * c, r * sp * sn, r * z);
+}
+// hit_sphere (intersection_taichi.py:15-36): nearest root in [t_min, t_max], else far root
+__device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, float t_max, float& root) {
+    V3 oc = o - xyz(sc);
+    float a = dot(d, d);
+    float half_b = dot(oc, d);
+    float cc = dot(oc, oc) - sc.w * sc.w;
+    float disc = half_b * half_b - a * cc;
+    if (!(disc >= 0.0f)) return false;
+    float sq = sqrtf(disc);
+    root = (-half_b - sq) / a;
+    if (root < t_min || t_max < root) {
+        root = (-half_b + sq) / a;
+        if (root < t_min || t_max < root) return false;
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- traversal
 struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf; };
 
@@ -513,6 +570,20 @@ void trace_kernel(TraceParams P) {
             hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         }
 
+        if (P.n_sph > 0 && !(qtype == Q_SHADOW && hit)) {
+            // analytic spheres after the triangles (ids n_tri + k), same rule as the oracle
+            float best = hit ? ht : tmax;
+            for (int k = 0; k < P.n_sph; ++k) {
+                float root;
+                if (sphere_hit(P.sph[k], o, d, kTMin, best, root)) {
+                    best = root;
+                    hid = P.n_tri + k;
+                    hit = true;
+                    if (qtype == Q_SHADOW) break;
+                }
+            }
+            ht = best;
+        }
         if (STATS) {
             t_b = __builtin_amdgcn_s_memtime();
             c_trav += t_b - t_a;
@@ -532,11 +603,52 @@ void trace_kernel(TraceParams P) {
             if (!hit) {
                 finished = true;
             } else {
-                float4 nm = P.tri_nm[hid];
-                const float* m = P.mats + 8 * __float_as_int(nm.w);
-                V3 n = xyz(nm);
+                V3 p = o + d * ht;                                         // ray.at
+                V3 ng;
+                int mid;
+                if (hid < P.n_tri) {
+                    float4 nm = P.tri_nm[hid];
+                    ng = xyz(nm);
+                    mid = __float_as_int(nm.w);
+                } else {                                                   // sphere: (p - c) / r
+                    float4 sc = P.sph[hid - P.n_tri];
+                    ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
+                    mid = P.sph_mat[hid - P.n_tri];
+                }
+                const float* m = P.mats + 8 * mid;
+                V3 n = ng;
                 if (m[4] == 0.0f && dot(n, neg(d)) < 0.0f) n = neg(n);   // shapes.py:101-102
-                if (m[3] != 0.0f) {                                        // tracing.py:129-139
+                if (m[5] == 2.0f || m[5] == 3.0f) {
+                    // specular BSDFs (build-added, config 3; bsdf_taichi.py:52-59, :69-86):
+                    // delta distributions, beta *= albedo, no NEE
+                    bool front = dot(d, ng) < 0.0f;
+                    V3 ns = front ? ng : neg(ng);
+                    V3 unit = normalize(d);
+                    V3 out;
+                    bool absorbed = false;
+                    if (m[5] == 2.0f) {
+                        out = reflect3(unit, ns);
+                        if (m[7] > 0.0f) out = out + random_in_unit_sphere(st) * m[7];
+                        absorbed = !(dot(out, ns) > 0.0f);
+                    } else {
+                        float ratio = front ? 1.0f / m[6] : m[6];
+                        float ct = -dot(unit, ns);
+                        ct = ct > 1.0f ? 1.0f : ct;
+                        float stn = sqrtf(1.0f - ct * ct);
+                        bool cannot = ratio * stn > 1.0f;
+                        if (cannot || schlick(ct, ratio) > rng_next(st)) out = reflect3(unit, ns);
+                        else out = refract3(unit, ns, ratio);
+                    }
+                    if (absorbed) {
+                        finished = true;
+                    } else {
+                        beta = beta * v3(m[0], m[1], m[2]);
+                        o = p;
+                        d = normalize(out);
+                        ++bounce;
+                        if (bounce >= P.depth) finished = true;
+                    }
+                } else if (m[3] != 0.0f) {                                 // tracing.py:129-139
                     float d1 = dot(neg(d), n);
                     if (d1 > 0.0f) {
                         V3 lc = v3(P.dl_r, P.dl_g, P.dl_b);
@@ -549,7 +661,6 @@ void trace_kernel(TraceParams P) {
                     float u1 = rng_next(st);
                     wi = to_world(n, cosine_hemisphere(u0, u1));
                     float pdf = fabsf(dot(n, wi)) * kInvPi;
-                    V3 p = o + d * ht;                                     // ray.at
                     V3 att = v3(m[0], m[1], m[2]);
                     float cw = dot(n, wi);
                     float dz = cw > 0.0f ? cw : 0.0f;
