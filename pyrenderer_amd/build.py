@@ -20,7 +20,9 @@ ARCH = os.environ.get("PRT_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: f32 results must match oracle/prt_oracle.c bit for bit
 # (DESIGN.md "Arithmetic contract"); division/sqrt stay correctly rounded
 # (hipcc's default -fhip-fp32-correctly-rounded-divide-sqrt).
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+# -fno-slp-vectorize: packed-f32 SLP code pins constant pairs in VGPRs (spills at the
+# occupancy targets) and is an anti-lever on CDNA4 (cdna_hip_programming.md, packed f32 VALU).
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize",
          f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 
 

@@ -263,4 +263,90 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     return true;
 }
 
+namespace {
+
+struct Child {
+    float lo[3], hi[3];
+    int32_t ref;
+    bool empty;
+};
+
+inline int32_t ref_of(const float* n2, int side) {
+    int32_t r;
+    std::memcpy(&r, n2 + 12 + side, 4);
+    return r;
+}
+
+inline Child child_of(const float* n2, int side) {
+    Child c;
+    const float* b = n2 + 6 * side;
+    c.lo[0] = b[0]; c.hi[0] = b[1]; c.lo[1] = b[2]; c.hi[1] = b[3]; c.lo[2] = b[4]; c.hi[2] = b[5];
+    c.ref = ref_of(n2, side);
+    c.empty = !(c.lo[0] <= c.hi[0]);
+    return c;
+}
+
+inline double child_area(const Child& c) {
+    double dx = (double)c.hi[0] - c.lo[0], dy = (double)c.hi[1] - c.lo[1], dz = (double)c.hi[2] - c.lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+}  // namespace
+
+void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
+    // Each BVH4 node takes a BVH2 node's two children and repeatedly opens the
+    // inner child with the largest surface area until it holds four children.
+    struct Item { int32_t b2node; int32_t slot; int32_t depth; };
+    std::vector<Item> work;
+    out->nodes.clear();
+    out->nodes.resize(32, 0.0f);
+    out->n_nodes = 1;
+    out->depth = 0;
+    work.push_back({0, 0, 0});
+    while (!work.empty()) {
+        Item it = work.back();
+        work.pop_back();
+        const float* n2 = b2.nodes.data() + (size_t)it.b2node * 16;
+        std::vector<Child> ch;
+        for (int side = 0; side < 2; ++side) {
+            Child c = child_of(n2, side);
+            if (!c.empty) ch.push_back(c);
+        }
+        while (ch.size() < 4) {
+            int best = -1;
+            double ba = -1.0;
+            for (size_t k = 0; k < ch.size(); ++k)
+                if (ch[k].ref >= 0 && child_area(ch[k]) > ba) { ba = child_area(ch[k]); best = (int)k; }
+            if (best < 0) break;
+            const float* m = b2.nodes.data() + (size_t)ch[best].ref * 16;
+            Child a = child_of(m, 0), b = child_of(m, 1);
+            ch.erase(ch.begin() + best);
+            if (!a.empty) ch.push_back(a);
+            if (!b.empty) ch.push_back(b);
+        }
+        float* f = out->nodes.data() + (size_t)it.slot * 32;
+        for (int k = 0; k < 4; ++k) {
+            bool ok = k < (int)ch.size();
+            for (int a = 0; a < 3; ++a) {
+                f[(2 * a) * 4 + k] = ok ? ch[k].lo[a] : INFINITY;
+                f[(2 * a + 1) * 4 + k] = ok ? ch[k].hi[a] : INFINITY;
+            }
+            int32_t ref = 0;
+            if (ok) {
+                if (ch[k].ref >= 0) {
+                    ref = (int32_t)out->n_nodes++;
+                    out->nodes.resize((size_t)out->n_nodes * 32, 0.0f);
+                    f = out->nodes.data() + (size_t)it.slot * 32;   // storage may have moved
+                    work.push_back({ch[k].ref, ref, it.depth + 1});
+                } else {
+                    ref = ch[k].ref;
+                }
+            }
+            std::memcpy(f + 24 + k, &ref, 4);
+        }
+        out->depth = std::max(out->depth, it.depth);
+    }
+    out->stack_need = 3 * (out->depth + 1) + 1;
+}
+
 }  // namespace prt

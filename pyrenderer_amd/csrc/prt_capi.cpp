@@ -65,11 +65,15 @@ struct Scene {
     int occ[32] = {0};               // blocks/CU per (variant, stats) once queried
     int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
-    DevBuf nodes, tris, tri_nm, mats, light_v, light_off, sph, sph_mat;
+    DevBuf nodes, nodes4, tris, tri_nm, mats, light_v, light_off, sph, sph_mat;
+    int64_t n_node4_f4 = 0;
+    int32_t depth4 = 0;
+    int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
     int64_t n_sph = 0;
     DevBuf tiles, buf, acc, work, stats;
     hipStream_t stream = nullptr;
     std::vector<hipEvent_t> ev;   // start/stop pairs of the last timed call
+    std::vector<uint32_t> tile_host;
     int ev_used = 0;
     size_t chunk_bytes = (size_t)4 << 30;  // per-sample buffer budget (HBM is 288 GB)
     size_t device_bytes = 0;
@@ -91,7 +95,7 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->nodes, &s->tris, &s->tri_nm, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
+    for (DevBuf* b : {&s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
                       &s->tiles, &s->buf, &s->acc, &s->work, &s->stats})
         b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
@@ -104,7 +108,9 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
     if (!s) return fail(PRT_ERR_ARG, "scene is NULL");
     if (!cam) return fail(PRT_ERR_ARG, "cam is NULL");
     if (W < 2 || H < 2) return fail(PRT_ERR_ARG, "W and H must be >= 2 (u = (x + r) / (W - 1))");
-    if (tw < 1 || th < 1 || (int64_t)tw * th > (1 << 20)) return fail(PRT_ERR_ARG, "bad tile size");
+    if (tw < 1 || th < 1 || (tw & (tw - 1)) || (th & (th - 1)) || (int64_t)tw * th < 64 || (int64_t)tw * th > (1 << 20))
+        return fail(PRT_ERR_ARG, "tile width/height must be powers of two with 64 <= tw*th <= 2^20");
+    if (W > 65535 || H > 65535) return fail(PRT_ERR_ARG, "frame larger than 65535 pixels per side");
     if (n_tiles < 0 || (n_tiles > 0 && !tile_ids)) return fail(PRT_ERR_ARG, "bad tile list");
     if (spp < 0 || depth < 0) return fail(PRT_ERR_ARG, "spp and depth must be >= 0");
     int tiles_x = (W + tw - 1) / tw, tiles_y = (H + th - 1) / th;
@@ -118,15 +124,22 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
 // LDS-resident scene: BVH + triangles small enough to sit beside the stack
 constexpr int64_t kLdsSceneBytes = 24 * 1024;
 bool lds_fits(const Scene* s) { return 16 * (s->n_node_f4 + s->n_tri_f4) <= kLdsSceneBytes; }
-int default_variant(const Scene* s) { return lds_fits(s) ? prt::kVarWWLds6 : prt::kVarWW; }
+bool lds_fits4(const Scene* s) { return 16 * (s->n_node4_f4 + s->n_tri_f4) <= kLdsSceneBytes; }
+int default_variant(const Scene* s) { return (s->stack4 && lds_fits4(s)) ? prt::kVarWW4Lds6 : prt::kVarWW; }
 
 // Enqueue the whole render of a tile set on `stream`, result in d_acc.
 int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,
                    int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc, hipStream_t stream) {
     const int64_t n_slots = (int64_t)n_tiles * tw * th;
     if (n_slots == 0) return PRT_OK;
-    HIP_TRY(s->tiles.ensure(sizeof(int32_t) * (size_t)n_tiles));
-    HIP_TRY(hipMemcpyAsync(s->tiles.p, tile_ids, sizeof(int32_t) * (size_t)n_tiles, hipMemcpyHostToDevice, stream));
+    // per-tile pixel origins (x0 << 16 | y0), staged in a pinned host buffer
+    const int tiles_x = (W + tw - 1) / tw;
+    if ((int64_t)s->tile_host.size() < n_tiles) s->tile_host.resize((size_t)n_tiles);
+    for (int i = 0; i < n_tiles; ++i)
+        s->tile_host[(size_t)i] = ((uint32_t)((tile_ids[i] % tiles_x) * tw) << 16) | (uint32_t)((tile_ids[i] / tiles_x) * th);
+    HIP_TRY(s->tiles.ensure(sizeof(uint32_t) * (size_t)n_tiles));
+    HIP_TRY(hipMemcpyAsync(s->tiles.p, s->tile_host.data(), sizeof(uint32_t) * (size_t)n_tiles, hipMemcpyHostToDevice,
+                           stream));
     if (spp == 0 || depth == 0) {
         HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots, stream));
         return PRT_OK;
@@ -151,8 +164,11 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.n_light = s->n_light;
     P.dl_r = s->direct_rgb[0]; P.dl_g = s->direct_rgb[1]; P.dl_b = s->direct_rgb[2];
     std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
-    P.W = W; P.H = H; P.tw = tw; P.th = th; P.tiles_x = (W + tw - 1) / tw;
-    P.tile_ids = (const int*)s->tiles.p;
+    P.W = W; P.H = H;
+    P.wm1 = (float)(W - 1); P.hm1 = (float)(H - 1);
+    P.log_tw = __builtin_ctz((unsigned)tw);
+    P.log_tpx = __builtin_ctz((unsigned)(tw * th));
+    P.tile_xy = (const uint32_t*)s->tiles.p;
     P.n_slots = (int)n_slots;
     P.depth = depth;
     P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
@@ -161,6 +177,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.stats = (unsigned long long*)s->stats.p;
     P.n_node_f4 = (int)s->n_node_f4;
     P.n_tri_f4 = (int)s->n_tri_f4;
+    int stack = s->stack;
     P.n_tri = (int)s->n_tri;
     P.n_sph = (int)s->n_sph;
     P.sph = (const float4*)s->sph.p;
@@ -168,9 +185,17 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFu);
     if (var == 0) var = default_variant(s);
     if (var < prt::kVarSplit || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
-    if (prt::variant_uses_lds(var) && !lds_fits(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
+    const bool b4 = prt::variant_uses_bvh4(var);
+    if (b4) {
+        if (s->stack4 == 0) return fail(PRT_ERR_ARG, "BVH4 too deep for the traversal stack variants");
+        P.nodes = (const float4*)s->nodes4.p;
+        P.n_node_f4 = (int)s->n_node4_f4;
+        stack = s->stack4;
+    }
+    if (prt::variant_uses_lds(var) && !(b4 ? lds_fits4(s) : lds_fits(s)))
+        return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
     int& occ = s->occ[2 * var + (stats ? 1 : 0)];
-    if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(s->stack, var, stats, prt::trace_smem_bytes(s->stack, var, P)));
+    if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(stack, var, stats, prt::trace_smem_bytes(stack, var, P)));
 
     int64_t n_chunks = (spp + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
@@ -191,7 +216,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
         HIP_TRY(hipMemsetAsync(s->work.p, 0, 16, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
-        HIP_TRY(prt::launch_trace(P, s->stack, var, grid, stats, stream));
+        HIP_TRY(prt::launch_trace(P, stack, var, grid, stats, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k + 1], stream));
         HIP_TRY(prt::launch_reduce((const float*)s->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0, stream));
     }
@@ -318,6 +343,14 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             lv[16 * k + 15] = bits_f(tri_mat[t]);
         }
         if ((rc = upload(s->nodes, bvh.nodes.data(), sizeof(float) * bvh.nodes.size(), &s->device_bytes))) break;
+        {
+            prt::Bvh4Host b4;
+            prt::collapse_bvh4(bvh, &b4);
+            s->depth4 = b4.depth;
+            s->n_node4_f4 = (int64_t)b4.nodes.size() / 4;
+            s->stack4 = b4.stack_need <= 64 ? prt::stack_variant(b4.stack_need - 1) : 0;
+            if ((rc = upload(s->nodes4, b4.nodes.data(), sizeof(float) * b4.nodes.size(), &s->device_bytes))) break;
+        }
         if ((rc = upload(s->tris, bvh.tris.data(), sizeof(float) * bvh.tris.size(), &s->device_bytes))) break;
         if ((rc = upload(s->tri_nm, nm.data(), sizeof(float) * nm.size(), &s->device_bytes))) break;
         if ((rc = upload(s->mats, mat, sizeof(float) * 8 * (size_t)n_mat, &s->device_bytes))) break;

@@ -35,6 +35,19 @@ struct BvhHost {
     double sah_cost = 0.0;
 };
 
+// BVH4 collapsed from the BVH2 (same triangle order and leaf encoding).
+// One node = 8 x float4 = 128 B, children in SoA so one node fetch tests
+// four boxes: f[0..5] = lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4];
+// f[6] = child refs (int bits); f[7] = unused.  Empty slots have lo = hi = +inf.
+constexpr int kNode4F4 = 8;
+struct Bvh4Host {
+    std::vector<float> nodes;      // n_nodes * 32
+    int64_t n_nodes = 0;
+    int32_t depth = 0;             // max root-to-leaf node count - 1
+    int32_t stack_need = 0;        // worst-case traversal stack entries (3 per level + sentinel)
+};
+void collapse_bvh4(const BvhHost& b2, Bvh4Host* out);
+
 // Builds a binned-SAH BVH2 over triangles (tri_v: n x 9 f32 world vertices).
 // Box padding keeps the slab test conservative w.r.t. Moller-Trumbore's own
 // rounding so traversal returns exactly the brute-force closest hit.

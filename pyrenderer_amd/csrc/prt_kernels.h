@@ -7,7 +7,7 @@ namespace prt {
 
 // Everything one trace launch needs, passed by value as the kernel argument.
 struct TraceParams {
-    const float4* nodes;      // BVH2, 4 float4 per node (prt_internal.h)
+    const float4* nodes;      // BVH2 (4 float4 per node) or BVH4 (8 float4 per node), prt_internal.h
     const float4* tris;       // BVH order, 3 float4 per triangle: (v0,id) (e1,0) (e2,0)
     const float4* tri_nm;     // original order: (face normal xyz, material id bits)
     const float* mats;        // n_mat x 8: rho.rgb, emit, sided, type, ior, roughness
@@ -17,8 +17,9 @@ struct TraceParams {
     float dl_r, dl_g, dl_b;   // directly-hit light colour (core/tracing.py:120)
     float cam[24];            // packed camera (include/prt.h)
     int W, H;                 // full frame (u = (x + r) / (W - 1))
-    int tw, th, tiles_x;      // tile geometry
-    const int* tile_ids;      // tiles of this launch
+    float wm1, hm1;           // (float)(W - 1), (float)(H - 1)
+    int log_tw, log_tpx;      // log2(tile width), log2(tile pixels): tiles are powers of two, >= 64 px
+    const uint32_t* tile_xy;  // per tile of this launch: (x0 << 16) | y0
     int n_slots;              // n_tiles * tw * th
     int s0;                   // first sample index of this chunk
     int depth;
@@ -43,8 +44,15 @@ constexpr int kVarWWLds = 5;       // while-while + LDS-resident scene
 constexpr int kVarWWLds5 = 6;      // ... compiled for >= 5 waves per SIMD
 constexpr int kVarWWLds6 = 7;      // ... compiled for >= 6 waves per SIMD
 constexpr int kVarWW5 = 8;         // while-while, global scene, >= 5 waves per SIMD
-constexpr int kVarLast = 8;
+constexpr int kVarWW4 = 9;         // while-while over the BVH4, global scene
+constexpr int kVarWW4Lds = 10;     // ... LDS-resident scene
+constexpr int kVarWW4Lds6 = 11;    // ... LDS-resident scene, >= 6 waves per SIMD
+constexpr int kVarWW4ParkLds6 = 12; // BVH4 + path state parked in LDS during traversal, LDS scene, >= 6 waves
+constexpr int kVarWW4ParkLds7 = 13; // ... >= 7 waves
+constexpr int kVarWW4Park5 = 14;    // BVH4 + parked state, global scene, >= 5 waves
+constexpr int kVarLast = 14;
 bool variant_uses_lds(int var);
+bool variant_uses_bvh4(int var);
 
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);

@@ -202,11 +202,14 @@ __device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, f
 struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf; };
 
 // Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
-__device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 o, V3 inv,
+__device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 oi, V3 inv,
                                      float tmin, float tmax, float& tn) {
-    float ax = (lx - o.x) * inv.x, bx = (hx - o.x) * inv.x;
-    float ay = (ly - o.y) * inv.y, by = (hy - o.y) * inv.y;
-    float az = (lz - o.z) * inv.z, bz = (hz - o.z) * inv.z;
+    // t = (lo - o) / d evaluated as fma(lo, 1/d, -o/d): pruning only, so the
+    // few-ulp error of the estimate is covered by the box padding (~1e-6 of the
+    // scene scale, >> |o/d| ulp) and the 1+2*gamma3 factor on t_far.
+    float ax = __builtin_fmaf(lx, inv.x, -oi.x), bx = __builtin_fmaf(hx, inv.x, -oi.x);
+    float ay = __builtin_fmaf(ly, inv.y, -oi.y), by = __builtin_fmaf(hy, inv.y, -oi.y);
+    float az = __builtin_fmaf(lz, inv.z, -oi.z), bz = __builtin_fmaf(hz, inv.z, -oi.z);
     float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
     float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * kGamma;
     tfar = fminf(tfar, tmax * kGamma);
@@ -241,7 +244,8 @@ __device__ __forceinline__ bool mt(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, fl
 template <bool ANY, bool STATS>
 __device__ __forceinline__ bool traverse(const TraceParams& P, V3 o, V3 d, float tmin, float tmax, int* lstack,
                                          int& hit_id, float& hit_t, Counters& cn) {
-    V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    V3 oi = o * inv;
     float best = tmax;
     int best_id = -1;
     int sp = 0;
@@ -252,8 +256,8 @@ __device__ __forceinline__ bool traverse(const TraceParams& P, V3 o, V3 d, float
             float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
             if (STATS) cn.nodes++;
             float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tmin, best, tr);
+            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
+            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
             int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
             if (hl && hr) {
                 bool lf = tl <= tr;
@@ -321,7 +325,8 @@ template <bool STATS>
 __device__ __forceinline__ bool traverse_u(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                            V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
                                            float& hit_t, Counters& cn) {
-    V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    V3 oi = o * inv;
     float best = tmax;
     int best_id = -1;
     int sp = 0;
@@ -332,8 +337,8 @@ __device__ __forceinline__ bool traverse_u(const float4* __restrict__ nodes, con
             float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
             if (STATS) cn.nodes++;
             float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tmin, best, tr);
+            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
+            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
             int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
             if (hl && hr) {
                 bool lf = tl <= tr;
@@ -384,7 +389,8 @@ template <bool STATS>
 __device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                             V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
                                             float& hit_t, Counters& cn) {
-    V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    V3 oi = o * inv;
     float best = tmax;
     int best_id = -1;
     lstack[0] = kSentinel;
@@ -398,8 +404,8 @@ __device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, co
             float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
             if (STATS) { cn.nodes++; cn.it_inner++; }
             float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, o, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, o, inv, tmin, best, tr);
+            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
+            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
             int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
             if (!hl && !hr) {
                 cur = lstack[sp * kBlock];
@@ -449,6 +455,97 @@ __device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, co
     return best_id >= 0;
 }
 
+// While-while over the BVH4 (prt_internal.h): one node fetch tests four child
+// boxes; hit children are ordered near-to-far with a 5-comparator network, the
+// nearest is visited next and the others pushed far-first.
+__device__ __forceinline__ void cswap(float& ta, int& ra, float& tb, int& rb) {
+    bool sw = tb < ta;
+    float t = sw ? tb : ta;
+    tb = sw ? ta : tb;
+    ta = t;
+    int r = sw ? rb : ra;
+    rb = sw ? ra : rb;
+    ra = r;
+}
+
+template <bool STATS>
+__device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
+                                             V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
+                                             float& hit_t, Counters& cn) {
+    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    V3 oi = o * inv;
+    float best = tmax;
+    int best_id = -1;
+    lstack[0] = kSentinel;
+    int sp = 0;
+    int cur = 0;
+    int leaf = 0;
+    do {
+        while (cur >= 0 && cur != kSentinel) {
+            const float4* nd = nodes + (size_t)cur * 8;
+            float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5], rf = nd[6];
+            if (STATS) { cn.nodes++; cn.it_inner++; }
+            float t0, t1, t2, t3;
+            bool h0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, oi, inv, tmin, best, t0);
+            bool h1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, oi, inv, tmin, best, t1);
+            bool h2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, oi, inv, tmin, best, t2);
+            bool h3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, oi, inv, tmin, best, t3);
+            int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z), r3 = __float_as_int(rf.w);
+            t0 = h0 ? t0 : INFINITY;
+            t1 = h1 ? t1 : INFINITY;
+            t2 = h2 ? t2 : INFINITY;
+            t3 = h3 ? t3 : INFINITY;
+            int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
+            cswap(t0, r0, t1, r1);
+            cswap(t2, r2, t3, r3);
+            cswap(t0, r0, t2, r2);
+            cswap(t1, r1, t3, r3);
+            cswap(t1, r1, t2, r2);
+            if (nh == 0) {
+                cur = lstack[sp * kBlock];
+                --sp;
+            } else {
+                cur = r0;
+                if (nh > 3) { ++sp; lstack[sp * kBlock] = r3; }
+                if (nh > 2) { ++sp; lstack[sp * kBlock] = r2; }
+                if (nh > 1) { ++sp; lstack[sp * kBlock] = r1; }
+            }
+            if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
+                leaf = cur;
+                cur = lstack[sp * kBlock];
+                --sp;
+            }
+            if (!__any(leaf >= 0)) break;
+        }
+        while (leaf < 0) {
+            int v = -leaf - 1;
+            int first = v >> 3, cnt = (v & 7) + 1;
+            if (STATS) cn.it_leaf++;
+            for (int k = 0; k < cnt; ++k) {
+                const float4* tp = tris + (size_t)(first + k) * 3;
+                float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+                int id = __float_as_int(q0.w);
+                float t;
+                if (STATS) cn.tris++;
+                if (mt_u(xyz(q0), xyz(q1), xyz(q2), o, d, tmin, best, id, best_id, any, t)) {
+                    best = t;
+                    best_id = id;
+                    if (any) { cur = kSentinel; break; }
+                }
+            }
+            if (any && best_id >= 0) { leaf = 0; break; }
+            leaf = cur;
+            if (cur < 0) {
+                cur = lstack[sp * kBlock];
+                --sp;
+            }
+        }
+    } while (cur != kSentinel || leaf < 0);
+    hit_id = best_id;
+    hit_t = best;
+    return best_id >= 0;
+}
+
 enum : int { Q_EXT = 0, Q_SHADOW = 1 };
 
 template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
@@ -456,12 +553,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_wa
 void trace_kernel(TraceParams P) {
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
+    // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
+    // while the lane traverses, so traversal registers do not add to it.
+    constexpr int kParkF4 = (VAR == 4) ? 3 * kBlock : 0;
     int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
+    float4* park = smem + kStackWords * kBlock / 4 + threadIdx.x;
     const float4* g_nodes = P.nodes;
     const float4* g_tris = P.tris;
     if (SCENE_LDS) {
         // small scene: copy BVH + triangles into LDS once per persistent block
-        float4* sn = smem + kStackWords * kBlock / 4;
+        float4* sn = smem + kStackWords * kBlock / 4 + kParkF4;
         float4* st4 = sn + P.n_node_f4;
         for (int i = threadIdx.x; i < P.n_node_f4; i += kBlock) sn[i] = P.nodes[i];
         for (int i = threadIdx.x; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
@@ -470,7 +571,6 @@ void trace_kernel(TraceParams P) {
         g_tris = st4;
     }
     const int lane = threadIdx.x & 63;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 
     // wave-uniform work queue [q_next, q_end)
     uint32_t q_next = 0, q_end = 0;
@@ -485,7 +585,7 @@ void trace_kernel(TraceParams P) {
     float tmax = kTMax;
     Counters cn = {0, 0, 0, 0, 0, 0};
     uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
-    const uint32_t tile_px = (uint32_t)(P.tw * P.th);
+    uint32_t chunk_s = 0;   // wave-uniform: sample index (within the launch) of the current chunk
 
     // diagnostic (STATS) wave-level clocks: refill / traversal / shading, iterations, active lanes
     uint64_t c_refill = 0, c_trav = 0, c_shade = 0, n_iter = 0, n_active = 0;
@@ -505,34 +605,47 @@ void trace_kernel(TraceParams P) {
                 } else {
                     q_next = base;
                     q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
+                    // n_slots is a multiple of 64 (tile sizes are powers of two >= 64 px),
+                    // so a chunk never straddles two samples: one scalar division per chunk
+                    chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
                 }
                 avail = q_end - q_next;
             }
             if (avail == 0) break;
-            uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             uint32_t need = (uint32_t)__popcll(idle);
             uint32_t take = need < avail ? need : avail;
             if (((idle >> lane) & 1ull) && rank < take) {
                 item = (int)(q_next + rank);
-                // start a new sample: main_taichi.py:89-95
-                uint32_t sl = (uint32_t)item / (uint32_t)P.n_slots;
-                uint32_t slot = (uint32_t)item - sl * (uint32_t)P.n_slots;
-                uint32_t tk = slot / tile_px, loc = slot - tk * tile_px;
-                int tid = P.tile_ids[tk];
-                int x = (tid % P.tiles_x) * P.tw + (int)(loc % (uint32_t)P.tw);
-                int y = (tid / P.tiles_x) * P.th + (int)(loc / (uint32_t)P.tw);
+                // start a new sample: main_taichi.py:89-95.  Uniform inputs are
+                // laundered through SGPR asm so the compiler cannot hoist their
+                // VALU-derived values out of the loop (they would pin VGPRs).
+                int W = P.W, H = P.H, log_tw = P.log_tw, log_tpx = P.log_tpx;
+                float wm1 = P.wm1, hm1 = P.hm1;
+                asm volatile("" : "+s"(W), "+s"(H), "+s"(log_tw), "+s"(log_tpx), "+s"(wm1), "+s"(hm1));
+                uint32_t slot = (uint32_t)item - chunk_s * (uint32_t)P.n_slots;
+                uint32_t tk = slot >> log_tpx, loc = slot & ((1u << log_tpx) - 1u);
+                uint32_t xy0 = P.tile_xy[tk];
+                int x = (int)(xy0 >> 16) + (int)(loc & ((1u << log_tw) - 1u));
+                int y = (int)(xy0 & 0xFFFFu) + (int)(loc >> log_tw);
                 L = v3(0, 0, 0);
-                if (x >= P.W || y >= P.H) {
+                if (x >= W || y >= H) {
                     float* out = P.out + (size_t)item * 3;
                     out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
                     item = -2;  // served, nothing to trace this iteration
                 } else {
-                    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)P.W + (uint32_t)x, (uint32_t)P.s0 + sl);
+                    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)W + (uint32_t)x, (uint32_t)P.s0 + chunk_s);
                     float r0 = rng_next(st);
-                    float u = ((float)x + r0) / (float)(P.W - 1);
+                    float u = ((float)x + r0) / wm1;
                     float r1 = rng_next(st);
-                    float vv = ((float)y + r1) / (float)(P.H - 1);
-                    gen_ray(P.cam, u, vv, st, o, d);
+                    float vv = ((float)y + r1) / hm1;
+                    float cam[24];
+#pragma unroll
+                    for (int i = 0; i < 20; ++i) {
+                        cam[i] = P.cam[i];
+                        asm volatile("" : "+s"(cam[i]));
+                    }
+                    gen_ray(cam, u, vv, st, o, d);
                     beta = v3(1, 1, 1);
                     bounce = 0;
                     qtype = Q_EXT;
@@ -566,8 +679,22 @@ void trace_kernel(TraceParams P) {
             else hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
         } else if (VAR == 1) {
             hit = traverse_u<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
-        } else {
+        } else if (VAR == 2) {
             hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+        } else if (VAR == 3) {
+            hit = traverse_ww4<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+        } else {
+            park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
+            park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
+            park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
+            asm volatile("" ::: "memory");
+            hit = traverse_ww4<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+            asm volatile("" ::: "memory");
+            float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
+            beta = v3(k0.x, k0.y, k0.z);
+            L = v3(k0.w, k1.x, k1.y);
+            pend = v3(k1.z, k1.w, k2.x);
+            wi = v3(k2.y, k2.z, k2.w);
         }
 
         if (P.n_sph > 0 && !(qtype == Q_SHADOW && hit)) {
@@ -777,7 +904,13 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
     X(kVarWWLds, 2, true, 1)                              \
     X(kVarWWLds5, 2, true, 5)                             \
     X(kVarWWLds6, 2, true, 6)                             \
-    X(kVarWW5, 2, false, 5)
+    X(kVarWW5, 2, false, 5)                               \
+    X(kVarWW4, 3, false, 1)                               \
+    X(kVarWW4Lds, 3, true, 1)                             \
+    X(kVarWW4Lds6, 3, true, 6)                            \
+    X(kVarWW4ParkLds6, 4, true, 6)                        \
+    X(kVarWW4ParkLds7, 4, true, 7)                        \
+    X(kVarWW4Park5, 4, false, 5)
 
 template <int STACK, bool STATS>
 static hipError_t launch_var(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream) {
@@ -801,8 +934,18 @@ bool variant_uses_lds(int var);
 // entries needed: one per level (<= depth) plus the while-while sentinel
 int stack_variant(int depth) { return depth + 1 <= 10 ? 10 : depth + 1 <= 16 ? 16 : depth + 1 <= 32 ? 32 : 64; }
 
+static bool variant_parks(int var) {
+    switch (var) {
+#define X(id, trav, lds, wpe) case id: return trav == 4;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
     size_t b = (size_t)stack * kBlock * sizeof(int);
+    if (variant_parks(var)) b += 48 * (size_t)kBlock;
     if (variant_uses_lds(var)) b += 16 * (size_t)(P.n_node_f4 + P.n_tri_f4);
     return b;
 }
@@ -834,6 +977,15 @@ static int occ_var(int var, size_t smem) {
         default: break;
     }
     return n;
+}
+
+bool variant_uses_bvh4(int var) {
+    switch (var) {
+#define X(id, trav, lds, wpe) case id: return trav >= 3;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
 }
 
 bool variant_uses_lds(int var) {

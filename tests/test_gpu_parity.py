@@ -184,3 +184,15 @@ def test_specular_scene_matches_oracle(rough):
     rmse, same = _compare(g, o, 4)
     assert rmse < TOL_RMSE, rmse
     assert same >= 0.999, same
+
+
+def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
+    """Every trace-kernel variant (split / unified / while-while, BVH2 / BVH4,
+    global / LDS scene, occupancy targets) renders the same bits as the oracle."""
+    from pyrenderer_amd.device_scene import interleaved_tiles
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    ids = interleaved_tiles(64, 64, 32)
+    o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
+    for v in range(1, 15):
+        g, _ = gpu_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
+        assert np.array_equal(g, o), v
