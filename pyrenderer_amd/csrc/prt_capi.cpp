@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -33,6 +34,33 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
+
+// rotate_to / rotate_z_to rows (mathematics/mat4_taichi.py:9-52) for a normal,
+// in the kernel's f32 arithmetic (this file is compiled with -ffp-contract=off):
+// rows (x, z, v) with v = normalize(n), x = normalize(v x (0,1,0)), z = normalize(x x v).
+struct F3 { float x, y, z; };
+F3 f3_norm(F3 a) {
+    float l = std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z);
+    return F3{a.x / l, a.y / l, a.z / l};
+}
+F3 f3_cross(F3 a, F3 b) { return F3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+void frame_rows(F3 n, float* out12) {
+    F3 v = f3_norm(n);
+    F3 r1, r2, r3;
+    if (v.y == 1.0f) {
+        r1 = F3{1, 0, 0}; r2 = F3{0, 0, 1}; r3 = F3{0, 1, 0};
+    } else if (v.y == -1.0f) {
+        r1 = F3{1, 0, 0}; r2 = F3{0, 0, 1}; r3 = F3{0, -1, 0};
+    } else {
+        F3 x = f3_norm(f3_cross(v, F3{0.0f, 1.0f, 0.0f}));
+        F3 z = f3_norm(f3_cross(x, v));
+        r1 = x; r2 = z; r3 = v;
+    }
+    const F3 rows[3] = {r1, r2, r3};
+    for (int k = 0; k < 3; ++k) {
+        out12[4 * k] = rows[k].x; out12[4 * k + 1] = rows[k].y; out12[4 * k + 2] = rows[k].z; out12[4 * k + 3] = 0.0f;
+    }
+}
 
 // stats words: nodes, tris, ext, shadow (public) + diagnostic wave clocks
 // (refill, traversal, shading), wave iterations, active lanes at traversal
@@ -65,7 +93,7 @@ struct Scene {
     int occ[32] = {0};               // blocks/CU per (variant, stats) once queried
     int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
-    DevBuf nodes, nodes4, tris, tri_nm, mats, light_v, light_off, sph, sph_mat;
+    DevBuf nodes, nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
     int64_t n_node4_f4 = 0;
     int32_t depth4 = 0;
     int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
@@ -95,7 +123,7 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
+    for (DevBuf* b : {&s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
                       &s->tiles, &s->buf, &s->acc, &s->work, &s->stats})
         b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
@@ -158,6 +186,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.nodes = (const float4*)s->nodes.p;
     P.tris = (const float4*)s->tris.p;
     P.tri_nm = (const float4*)s->tri_nm.p;
+    P.tri_frame = (const float4*)s->tri_frame.p;
     P.mats = (const float*)s->mats.p;
     P.light_v = (const float4*)s->light_v.p;
     P.light_off = (const int*)s->light_off.p;
@@ -330,6 +359,12 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             nm[4 * i] = tri_n[3 * i]; nm[4 * i + 1] = tri_n[3 * i + 1]; nm[4 * i + 2] = tri_n[3 * i + 2];
             nm[4 * i + 3] = bits_f(tri_mat[i]);
         }
+        std::vector<float> fr((size_t)std::max<int64_t>(n_tri, 1) * 24, 0.0f);
+        for (int64_t i = 0; i < n_tri; ++i) {
+            F3 nn{tri_n[3 * i], tri_n[3 * i + 1], tri_n[3 * i + 2]};
+            frame_rows(nn, fr.data() + 24 * i);
+            frame_rows(F3{-nn.x, -nn.y, -nn.z}, fr.data() + 24 * i + 12);
+        }
         int n_lt = light_off[n_light];
         std::vector<float> lv((size_t)n_lt * 16, 0.0f);
         for (int k = 0; k < n_lt; ++k) {
@@ -353,6 +388,7 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         }
         if ((rc = upload(s->tris, bvh.tris.data(), sizeof(float) * bvh.tris.size(), &s->device_bytes))) break;
         if ((rc = upload(s->tri_nm, nm.data(), sizeof(float) * nm.size(), &s->device_bytes))) break;
+        if ((rc = upload(s->tri_frame, fr.data(), sizeof(float) * fr.size(), &s->device_bytes))) break;
         if ((rc = upload(s->mats, mat, sizeof(float) * 8 * (size_t)n_mat, &s->device_bytes))) break;
         if ((rc = upload(s->light_v, lv.data(), sizeof(float) * lv.size(), &s->device_bytes))) break;
         if ((rc = upload(s->light_off, light_off, sizeof(int32_t) * (size_t)(n_light + 1), &s->device_bytes))) break;

@@ -10,6 +10,7 @@ struct TraceParams {
     const float4* nodes;      // BVH2 (4 float4 per node) or BVH4 (8 float4 per node), prt_internal.h
     const float4* tris;       // BVH order, 3 float4 per triangle: (v0,id) (e1,0) (e2,0)
     const float4* tri_nm;     // original order: (face normal xyz, material id bits)
+    const float4* tri_frame;  // original order: rotate_z_to rows (x, z, n) for the face normal and its negation
     const float* mats;        // n_mat x 8: rho.rgb, emit, sided, type, ior, roughness
     const float4* light_v;    // per light triangle: V0, V1, V2, (normal xyz, material id bits)
     const int* light_off;     // n_light + 1 prefix offsets into light triangles

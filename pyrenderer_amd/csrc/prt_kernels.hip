@@ -743,8 +743,8 @@ void trace_kernel(TraceParams P) {
                     mid = P.sph_mat[hid - P.n_tri];
                 }
                 const float* m = P.mats + 8 * mid;
-                V3 n = ng;
-                if (m[4] == 0.0f && dot(n, neg(d)) < 0.0f) n = neg(n);   // shapes.py:101-102
+                const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;   // shapes.py:101-102
+                const V3 n = flip ? neg(ng) : ng;
                 if (m[5] == 2.0f || m[5] == 3.0f) {
                     // specular BSDFs (build-added, config 3; bsdf_taichi.py:52-59, :69-86):
                     // delta distributions, beta *= albedo, no NEE
@@ -783,10 +783,19 @@ void trace_kernel(TraceParams P) {
                     }
                     finished = true;
                 } else {
-                    // BSDFLambertian.scatter + frame (bsdf.py:29-34, shapes.py:105-108)
+                    // BSDFLambertian.scatter + frame (bsdf.py:29-34, shapes.py:105-108).
+                    // Triangles read rotate_z_to's rows precomputed on the host with the
+                    // same f32 arithmetic (per face and side); spheres build them here.
                     float u0 = rng_next(st);
                     float u1 = rng_next(st);
-                    wi = to_world(n, cosine_hemisphere(u0, u1));
+                    V3 l = cosine_hemisphere(u0, u1);
+                    if (hid < P.n_tri) {
+                        const float4* fr = P.tri_frame + ((size_t)hid * 2 + (flip ? 1 : 0)) * 3;
+                        float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
+                        wi = normalize(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
+                    } else {
+                        wi = to_world(n, l);
+                    }
                     float pdf = fabsf(dot(n, wi)) * kInvPi;
                     V3 att = v3(m[0], m[1], m[2]);
                     float cw = dot(n, wi);
