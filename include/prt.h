@@ -40,11 +40,13 @@ extern "C" {
 /* render flags */
 #define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
 #define PRT_FLAG_TIME 0x2u   /* time the trace kernel with HIP events on its stream */
-/* trace-kernel variant in bits 8..11 (0 = automatic): 1 split closest/any-hit
- * traversal, 2 unified traversal, 3 unified + LDS-resident scene (small scenes).
- * All variants produce bit-identical images; the selector exists for A/B runs. */
+/* trace-kernel variant in bits 8..15 (0 = automatic; the numbering is the
+ * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: split / unified / while-while
+ * traversal, BVH2 / BVH4, global / LDS-resident scene, occupancy targets,
+ * phase-aligned scheduling).  All variants produce bit-identical images; the
+ * selector exists for A/B runs. */
 #define PRT_FLAG_VARIANT_SHIFT 8
-#define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFu) << PRT_FLAG_VARIANT_SHIFT)
+#define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFFu) << PRT_FLAG_VARIANT_SHIFT)
 
 /* material row (8 floats): rho.r rho.g rho.b emit sided type ior roughness */
 #define PRT_MAT_LAMBERT 0    /* core/bsdf.py:18-42 BSDFLambertian */

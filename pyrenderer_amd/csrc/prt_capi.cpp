@@ -90,7 +90,8 @@ struct Scene {
     int n_mat = 0;
     int cus = 0;
     int blocks_per_cu = 0;           // of the default variant
-    int occ[32] = {0};               // blocks/CU per (variant, stats) once queried
+    int occ[2 * (prt::kVarLast + 1)] = {0};  // blocks/CU per (variant, stats) once queried
+    int n_lt = 0;                    // emitter triangles
     int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
     DevBuf nodes, nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
@@ -151,9 +152,33 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
 
 // LDS-resident scene: BVH + triangles small enough to sit beside the stack
 constexpr int64_t kLdsSceneBytes = 24 * 1024;
-bool lds_fits(const Scene* s) { return 16 * (s->n_node_f4 + s->n_tri_f4) <= kLdsSceneBytes; }
-bool lds_fits4(const Scene* s) { return 16 * (s->n_node4_f4 + s->n_tri_f4) <= kLdsSceneBytes; }
-int default_variant(const Scene* s) { return (s->stack4 && lds_fits4(s)) ? prt::kVarWW4Lds6 : prt::kVarWW; }
+void scene_sizes(const Scene* s, bool bvh4, prt::TraceParams& P) {
+    P.n_node_f4 = (int)(bvh4 ? s->n_node4_f4 : s->n_node_f4);
+    P.n_tri_f4 = (int)s->n_tri_f4;
+    P.n_tri = (int)s->n_tri;
+    P.n_mat = s->n_mat;
+    P.n_lt = s->n_lt;
+    P.n_light = s->n_light;
+}
+bool lds_fits_var(const Scene* s, bool bvh4) {
+    prt::TraceParams P;
+    std::memset(&P, 0, sizeof(P));
+    scene_sizes(s, bvh4, P);
+    return (int64_t)prt::lds_scene_bytes(P) <= kLdsSceneBytes;
+}
+bool lds_fits(const Scene* s) { return lds_fits_var(s, false); }
+bool lds_fits4(const Scene* s) { return lds_fits_var(s, true); }
+// LDS-resident scene when it fits; the >= 6 waves/SIMD build when six blocks' LDS
+// still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
+int default_variant(const Scene* s) {
+    if (!s->stack4) return prt::kVarWW;
+    if (!lds_fits4(s)) return prt::kVarWW4;
+    prt::TraceParams P;
+    std::memset(&P, 0, sizeof(P));
+    scene_sizes(s, true, P);
+    size_t smem = prt::trace_smem_bytes(s->stack4, prt::kVarWW4Lds6, P);
+    return smem * 6 <= 160 * 1024 ? prt::kVarWW4PhLds6 : prt::kVarWW4Lds;
+}
 
 // Enqueue the whole render of a tile set on `stream`, result in d_acc.
 int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,
@@ -193,6 +218,18 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.n_light = s->n_light;
     P.dl_r = s->direct_rgb[0]; P.dl_g = s->direct_rgb[1]; P.dl_b = s->direct_rgb[2];
     std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
+    {
+        bool fin = true;
+        for (int i = 0; i < 20; ++i) fin = fin && std::isfinite(cam[i]);
+        P.cam_fast = fin && !(cam[19] > 0.0f) && cam[12] == 0.0f && cam[13] == 0.0f && cam[14] == 0.0f &&
+                     cam[15] == 1.0f;
+        const float rd2 = -cam[18];
+        for (int i = 0; i < 3; ++i) {
+            const float* c = cam + 4 * i;
+            P.cam_o[i] = 0.0f * c[0] + 0.0f * c[1] + 0.0f * c[2] + 1.0f * c[3];
+            P.cam_k[i] = rd2 * c[2];
+        }
+    }
     P.W = W; P.H = H;
     P.wm1 = (float)(W - 1); P.hm1 = (float)(H - 1);
     P.log_tw = __builtin_ctz((unsigned)tw);
@@ -204,14 +241,12 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.work = (uint32_t*)s->work.p;
     P.out = (float*)s->buf.p;
     P.stats = (unsigned long long*)s->stats.p;
-    P.n_node_f4 = (int)s->n_node_f4;
-    P.n_tri_f4 = (int)s->n_tri_f4;
+    scene_sizes(s, false, P);
     int stack = s->stack;
-    P.n_tri = (int)s->n_tri;
     P.n_sph = (int)s->n_sph;
     P.sph = (const float4*)s->sph.p;
     P.sph_mat = (const int*)s->sph_mat.p;
-    int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFu);
+    int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFFu);
     if (var == 0) var = default_variant(s);
     if (var < prt::kVarSplit || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
     const bool b4 = prt::variant_uses_bvh4(var);
@@ -366,6 +401,7 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             frame_rows(F3{-nn.x, -nn.y, -nn.z}, fr.data() + 24 * i + 12);
         }
         int n_lt = light_off[n_light];
+        s->n_lt = n_lt;
         std::vector<float> lv((size_t)n_lt * 16, 0.0f);
         for (int k = 0; k < n_lt; ++k) {
             int64_t t = light_tri[k];
@@ -407,10 +443,11 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         {
             prt::TraceParams Q;
             std::memset(&Q, 0, sizeof(Q));
-            Q.n_node_f4 = (int)s->n_node_f4;
-            Q.n_tri_f4 = (int)s->n_tri_f4;
             int var = default_variant(s);
-            s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(s->stack, var, false, prt::trace_smem_bytes(s->stack, var, Q)));
+            bool b4 = prt::variant_uses_bvh4(var);
+            scene_sizes(s, b4, Q);
+            int stk = b4 ? s->stack4 : s->stack;
+            s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(stk, var, false, prt::trace_smem_bytes(stk, var, Q)));
         }
         if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
     } while (0);

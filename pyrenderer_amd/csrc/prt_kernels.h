@@ -17,6 +17,11 @@ struct TraceParams {
     int n_light;
     float dl_r, dl_g, dl_b;   // directly-hit light colour (core/tracing.py:120)
     float cam[24];            // packed camera (include/prt.h)
+    // pinhole camera with an affine matrix (no aperture, last row (0,0,0,1), all finite):
+    // the ray origin M (0,0,0,1) and the constant terms rd.z * M[i][2] of gen_ray,
+    // evaluated on the host in the kernel's f32 order (camera_taichi.py:47-74)
+    int cam_fast;
+    float cam_o[3], cam_k[3];
     int W, H;                 // full frame (u = (x + r) / (W - 1))
     float wm1, hm1;           // (float)(W - 1), (float)(H - 1)
     int log_tw, log_tpx;      // log2(tile width), log2(tile pixels): tiles are powers of two, >= 64 px
@@ -30,6 +35,7 @@ struct TraceParams {
     float* out;               // n_items x 3 radiance, item = (s - s0) * n_slots + slot
     unsigned long long* stats;  // 4 counters (nodes, tris, ext queries, shadow queries)
     int n_node_f4, n_tri_f4;  // scene sizes in float4 (LDS-resident variant)
+    int n_mat, n_lt;          // materials (8 floats each), emitter triangles
     int n_tri;                // hit ids >= n_tri are spheres
     int n_sph;
     const float4* sph;        // center xyz, radius
@@ -51,12 +57,17 @@ constexpr int kVarWW4Lds6 = 11;    // ... LDS-resident scene, >= 6 waves per SIM
 constexpr int kVarWW4ParkLds6 = 12; // BVH4 + path state parked in LDS during traversal, LDS scene, >= 6 waves
 constexpr int kVarWW4ParkLds7 = 13; // ... >= 7 waves
 constexpr int kVarWW4Park5 = 14;    // BVH4 + parked state, global scene, >= 5 waves
-constexpr int kVarLast = 14;
+constexpr int kVarWW4PhLds6 = 15;   // BVH4, LDS scene, >= 6 waves, phase-aligned ext/shadow iterations
+constexpr int kVarWW4PhLds = 16;    // ... LDS scene, no occupancy target
+constexpr int kVarWW4Ph = 17;       // ... global scene
+constexpr int kVarWW4Ph5 = 18;      // ... global scene, >= 5 waves
+constexpr int kVarLast = 18;
 bool variant_uses_lds(int var);
 bool variant_uses_bvh4(int var);
 
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);
+size_t lds_scene_bytes(const TraceParams& P);  // LDS-resident scene + shading data
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);

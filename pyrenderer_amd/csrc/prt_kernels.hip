@@ -43,6 +43,10 @@ __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y 
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+// a / b is NaN (IEEE): a or b NaN, 0/0 or inf/inf
+__device__ __forceinline__ bool div_is_nan(float a, float b) {
+    return isnan(a) || isnan(b) || (a == 0.0f && b == 0.0f) || (isinf(a) && isinf(b));
+}
 // taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt)
 __device__ __forceinline__ V3 normalize(V3 a) {
     float l = sqrtf(dot(a, a));
@@ -551,24 +555,49 @@ enum : int { Q_EXT = 0, Q_SHADOW = 1 };
 template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel(TraceParams P) {
+    // VAR = traversal kind (0 split, 1 unified, 2 while-while BVH2, 3 while-while BVH4,
+    // 4 BVH4 + parked state) | 8 for phase-aligned scheduling (see below)
+    constexpr int TRAV = VAR & 7;
+    constexpr bool PHASE = (VAR & 8) != 0;
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
     // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
     // while the lane traverses, so traversal registers do not add to it.
-    constexpr int kParkF4 = (VAR == 4) ? 3 * kBlock : 0;
+    constexpr int kParkF4 = (TRAV == 4) ? 3 * kBlock : 0;
     int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
     float4* park = smem + kStackWords * kBlock / 4 + threadIdx.x;
     const float4* g_nodes = P.nodes;
     const float4* g_tris = P.tris;
+    const float4* s_nm = P.tri_nm;
+    const float4* s_fr = P.tri_frame;
+    const float* s_mats = P.mats;
+    const float4* s_lv = P.light_v;
+    const int* s_loff = P.light_off;
     if (SCENE_LDS) {
-        // small scene: copy BVH + triangles into LDS once per persistent block
+        // small scene: copy BVH + triangles, and the shading data (normals, frames,
+        // materials, emitters), into LDS once per persistent block
         float4* sn = smem + kStackWords * kBlock / 4 + kParkF4;
         float4* st4 = sn + P.n_node_f4;
+        float4* snm = st4 + P.n_tri_f4;
+        float4* sfr = snm + P.n_tri;
+        float4* smt = sfr + 6 * P.n_tri;
+        float4* slv = smt + 2 * P.n_mat;
+        int* slo = reinterpret_cast<int*>(slv + 4 * P.n_lt);
         for (int i = threadIdx.x; i < P.n_node_f4; i += kBlock) sn[i] = P.nodes[i];
         for (int i = threadIdx.x; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
+        for (int i = threadIdx.x; i < P.n_tri; i += kBlock) snm[i] = P.tri_nm[i];
+        for (int i = threadIdx.x; i < 6 * P.n_tri; i += kBlock) sfr[i] = P.tri_frame[i];
+        for (int i = threadIdx.x; i < 2 * P.n_mat; i += kBlock) smt[i] = reinterpret_cast<const float4*>(P.mats)[i];
+        for (int i = threadIdx.x; i < 4 * P.n_lt; i += kBlock) slv[i] = P.light_v[i];
+        for (int i = threadIdx.x; i <= P.n_light; i += kBlock) slo[i] = P.light_off[i];
         __syncthreads();
         g_nodes = sn;
         g_tris = st4;
+        s_nm = snm;
+        s_fr = sfr;
+        s_mats = reinterpret_cast<const float*>(smt);
+        s_lv = slv;
+        s_loff = slo;
     }
     const int lane = threadIdx.x & 63;
 
@@ -590,10 +619,20 @@ void trace_kernel(TraceParams P) {
     // diagnostic (STATS) wave-level clocks: refill / traversal / shading, iterations, active lanes
     uint64_t c_refill = 0, c_trav = 0, c_shade = 0, n_iter = 0, n_active = 0;
     uint64_t t_a = 0, t_b = 0;
+    // PHASE: the wave alternates extension and shadow iterations, so the costly
+    // shading code (run after extension queries only) and the refill execute
+    // with every busy lane at once instead of every iteration with about half.
+    // Lanes whose query kind does not match the wave's phase sit the iteration out.
+    bool last_shadow = false;
     while (true) {
         if (STATS) t_a = __builtin_amdgcn_s_memtime();
+        bool do_shadow = false;
+        if (PHASE) {
+            do_shadow = !last_shadow && __ballot(item >= 0 && qtype == Q_SHADOW) != 0;
+            last_shadow = do_shadow;
+        }
         // ---------------------------------------------------------- refill
-        uint64_t idle = __ballot(item < 0);
+        uint64_t idle = do_shadow ? 0ull : __ballot(item < 0);
         for (int round = 0; round < 2 && idle; ++round) {
             uint32_t avail = q_end - q_next;
             if (avail == 0 && !exhausted) {
@@ -639,13 +678,40 @@ void trace_kernel(TraceParams P) {
                     float u = ((float)x + r0) / wm1;
                     float r1 = rng_next(st);
                     float vv = ((float)y + r1) / hm1;
-                    float cam[24];
+                    if (P.cam_fast) {
+                        // gen_ray for a pinhole affine camera: the same operations minus
+                        // those with exactly known results (see TraceParams::cam_fast)
+                        float c[12], k[6];
 #pragma unroll
-                    for (int i = 0; i < 20; ++i) {
-                        cam[i] = P.cam[i];
-                        asm volatile("" : "+s"(cam[i]));
+                        for (int i = 0; i < 12; ++i) {
+                            c[i] = P.cam[i];
+                            asm volatile("" : "+s"(c[i]));
+                        }
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) {
+                            k[i] = P.cam_o[i];
+                            k[3 + i] = P.cam_k[i];
+                            asm volatile("" : "+s"(k[i]), "+s"(k[3 + i]));
+                        }
+                        float sd0 = P.cam[16], sd1 = P.cam[17];
+                        asm volatile("" : "+s"(sd0), "+s"(sd1));
+                        float rx = (u - 0.5f) * sd0 / 0.5f, ry = (vv - 0.5f) * sd1 / 0.5f;
+                        float f[3];
+#pragma unroll
+                        for (int i = 0; i < 3; ++i)
+                            f[i] = (((rx * c[4 * i] + ry * c[4 * i + 1]) + k[3 + i]) + c[4 * i + 3]) - k[i];
+                        float ln = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+                        o = v3(k[0], k[1], k[2]);
+                        d = v3(f[0] / ln, f[1] / ln, f[2] / ln);
+                    } else {
+                        float cam[24];
+#pragma unroll
+                        for (int i = 0; i < 20; ++i) {
+                            cam[i] = P.cam[i];
+                            asm volatile("" : "+s"(cam[i]));
+                        }
+                        gen_ray(cam, u, vv, st, o, d);
                     }
-                    gen_ray(cam, u, vv, st, o, d);
                     beta = v3(1, 1, 1);
                     bounce = 0;
                     qtype = Q_EXT;
@@ -661,6 +727,7 @@ void trace_kernel(TraceParams P) {
             continue;
         }
         if (item < 0) continue;
+        if (PHASE && (qtype == Q_SHADOW) != do_shadow) continue;
 
         // ------------------------------------------------------- one query
         int hid = -1;
@@ -674,14 +741,14 @@ void trace_kernel(TraceParams P) {
             n_iter++;
             n_active += (uint64_t)__popcll(__ballot(true));
         }
-        if (VAR == 0) {
+        if (TRAV == 0) {
             if (qtype == Q_EXT) hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
             else hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
-        } else if (VAR == 1) {
+        } else if (TRAV == 1) {
             hit = traverse_u<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
-        } else if (VAR == 2) {
+        } else if (TRAV == 2) {
             hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
-        } else if (VAR == 3) {
+        } else if (TRAV == 3) {
             hit = traverse_ww4<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         } else {
             park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
@@ -734,15 +801,16 @@ void trace_kernel(TraceParams P) {
                 V3 ng;
                 int mid;
                 if (hid < P.n_tri) {
-                    float4 nm = P.tri_nm[hid];
+                    float4 nm = s_nm[hid];
                     ng = xyz(nm);
                     mid = __float_as_int(nm.w);
                 } else {                                                   // sphere: (p - c) / r
+                    asm volatile("");   // keep the divisions in this branch (no if-conversion)
                     float4 sc = P.sph[hid - P.n_tri];
                     ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
                     mid = P.sph_mat[hid - P.n_tri];
                 }
-                const float* m = P.mats + 8 * mid;
+                const float* m = s_mats + 8 * mid;
                 const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;   // shapes.py:101-102
                 const V3 n = flip ? neg(ng) : ng;
                 if (m[5] == 2.0f || m[5] == 3.0f) {
@@ -790,7 +858,7 @@ void trace_kernel(TraceParams P) {
                     float u1 = rng_next(st);
                     V3 l = cosine_hemisphere(u0, u1);
                     if (hid < P.n_tri) {
-                        const float4* fr = P.tri_frame + ((size_t)hid * 2 + (flip ? 1 : 0)) * 3;
+                        const float4* fr = s_fr + ((size_t)hid * 2 + (flip ? 1 : 0)) * 3;
                         float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
                         wi = normalize(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
                     } else {
@@ -800,32 +868,36 @@ void trace_kernel(TraceParams P) {
                     V3 att = v3(m[0], m[1], m[2]);
                     float cw = dot(n, wi);
                     float dz = cw > 0.0f ? cw : 0.0f;
-                    V3 nb = v3(att.x * dz / pdf * kInvPi, att.y * dz / pdf * kInvPi, att.z * dz / pdf * kInvPi);
-                    if (isnan(nb.x) || isnan(nb.y) || isnan(nb.z)) {       // tracing.py:146-148
-                        pdf = 1e-4f;
-                        nb = v3(att.x * dz / pdf * kInvPi, att.y * dz / pdf * kInvPi, att.z * dz / pdf * kInvPi);
-                    }
+                    // tracing.py:146-148: if any component of att*dz/pdf*InvPi is NaN the
+                    // reference recomputes it with pdf = 1e-4.  (a / pdf) * InvPi is NaN
+                    // exactly when a / pdf is, so the condition is decided before dividing.
+                    V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
+                    if (div_is_nan(ad.x, pdf) || div_is_nan(ad.y, pdf) || div_is_nan(ad.z, pdf)) pdf = 1e-4f;
+                    V3 nb = v3(ad.x / pdf * kInvPi, ad.y / pdf * kInvPi, ad.z / pdf * kInvPi);
                     beta = beta * nb;
                     // sample_direct_lighting (tracing.py:92-108)
                     int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
-                    int lo = P.light_off[li];
-                    int f = rng_int(st, 0, P.light_off[li + 1] - lo - 1);
+                    int lo = s_loff[li];
+                    int f = rng_int(st, 0, s_loff[li + 1] - lo - 1);
                     float su = sqrtf(rng_next(st));
                     float sv = rng_next(st);
                     float a = su * (1.0f - sv);
                     float b = su * sv;
-                    const float4* lv = P.light_v + (size_t)(lo + f) * 4;
+                    const float4* lv = s_lv + (size_t)(lo + f) * 4;
                     float4 L0 = lv[0], L1 = lv[1], L2 = lv[2], LN = lv[3];
                     float c = 1.0f - a - b;
                     V3 p2 = (xyz(L0) * a + xyz(L1) * b) + xyz(L2) * c;
                     V3 n2 = xyz(LN);
                     V3 w = normalize(p2 - p);
-                    V3 w2 = normalize(p - p2);
                     float t_at = (p2.x - p.x) / w.x;
-                    float dot1 = dot(n, w), dot2 = dot(n2, w2);
+                    // w2 = normalize(p - p2) is -w bit for bit (round-to-nearest is sign
+                    // symmetric) up to the sign of zero components, so dot(n2, w2) =
+                    // -dot(n2, w) except for the sign of a zero result, which the
+                    // strict "> 0" test and the uses below cannot see.
+                    float dot1 = dot(n, w), dot2 = -dot(n2, w);
                     o = p;
                     if (dot1 > 0.0f && dot2 > 0.0f) {
-                        const float* em = P.mats + 8 * __float_as_int(LN.w);
+                        const float* em = s_mats + 8 * __float_as_int(LN.w);
                         V3 dd = p - p2;
                         float sl = dot(dd, dd);
                         V3 rad = v3(em[0] * dot1 * dot2 / sl, em[1] * dot1 * dot2 / sl, em[2] * dot1 * dot2 / sl);
@@ -904,7 +976,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
 
 }  // namespace
 
-// variant table: (traversal, LDS scene, min waves per SIMD); see prt_kernels.h
+// variant table: (traversal | 8 if phase-aligned, LDS scene, min waves per SIMD); see prt_kernels.h
 #define PRT_VARIANTS(X)                                   \
     X(kVarSplit, 0, false, 1)                             \
     X(kVarUnified, 1, false, 1)                           \
@@ -919,7 +991,11 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
     X(kVarWW4Lds6, 3, true, 6)                            \
     X(kVarWW4ParkLds6, 4, true, 6)                        \
     X(kVarWW4ParkLds7, 4, true, 7)                        \
-    X(kVarWW4Park5, 4, false, 5)
+    X(kVarWW4Park5, 4, false, 5)                        \
+    X(kVarWW4PhLds6, 11, true, 6)                        \
+    X(kVarWW4PhLds, 11, true, 1)                         \
+    X(kVarWW4Ph, 11, false, 1)                           \
+    X(kVarWW4Ph5, 11, false, 5)
 
 template <int STACK, bool STATS>
 static hipError_t launch_var(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream) {
@@ -945,17 +1021,22 @@ int stack_variant(int depth) { return depth + 1 <= 10 ? 10 : depth + 1 <= 16 ? 1
 
 static bool variant_parks(int var) {
     switch (var) {
-#define X(id, trav, lds, wpe) case id: return trav == 4;
+#define X(id, trav, lds, wpe) case id: return (trav & 7) == 4;
         PRT_VARIANTS(X)
 #undef X
         default: return false;
     }
 }
 
+size_t lds_scene_bytes(const TraceParams& P) {
+    return 16 * ((size_t)P.n_node_f4 + P.n_tri_f4 + 7 * (size_t)P.n_tri + 2 * (size_t)P.n_mat + 4 * (size_t)P.n_lt) +
+           4 * ((size_t)P.n_light + 1);
+}
+
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
     size_t b = (size_t)stack * kBlock * sizeof(int);
     if (variant_parks(var)) b += 48 * (size_t)kBlock;
-    if (variant_uses_lds(var)) b += 16 * (size_t)(P.n_node_f4 + P.n_tri_f4);
+    if (variant_uses_lds(var)) b += lds_scene_bytes(P);
     return b;
 }
 
@@ -990,7 +1071,7 @@ static int occ_var(int var, size_t smem) {
 
 bool variant_uses_bvh4(int var) {
     switch (var) {
-#define X(id, trav, lds, wpe) case id: return trav >= 3;
+#define X(id, trav, lds, wpe) case id: return (trav & 7) >= 3;
         PRT_VARIANTS(X)
 #undef X
         default: return false;

@@ -193,6 +193,20 @@ def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
     cam = cornell[1].convert_to_taichi_camera().packed()
     ids = interleaved_tiles(64, 64, 32)
     o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
-    for v in range(1, 15):
+    for v in range(1, 19):
         g, _ = gpu_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
         assert np.array_equal(g, o), v
+
+
+@pytest.mark.parametrize("mod", ["aperture", "projective"])
+def test_general_camera_matches_oracle(gpu_scene, oracle_scene, cornell, mod):
+    """The kernel's pinhole/affine camera shortcut must not change a bit, and the
+    general gen_ray (thin-lens draws, non-affine matrix) must match too."""
+    cam = cornell[1].convert_to_taichi_camera().packed().copy()
+    if mod == "aperture":
+        cam[19] = 1.0          # sensor_dim.w > 0: lens sample (camera_taichi.py:57-60)
+    else:
+        cam[12] = 1e-3         # last matrix row != (0, 0, 0, 1)
+    g = _gpu_frame(gpu_scene, cam, 40, 40, 2, 4, seed=3)
+    o = oracle_scene.render(cam, 40, 40, 2, 4, seed=3)
+    np.testing.assert_array_equal(g, o)

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", type=int, nargs="+", default=[1, 2, 3])
-    ap.add_argument("--scene", default="cornell", help="cornell | soup:N (random triangle soup of N tris in the box)")
+    ap.add_argument("--scene", default="cornell", help="cornell | cubes | soup:N (random triangle soup of N tris in the box)")
     a = ap.parse_args()
     from pyrenderer_amd._native import PRT_FLAG_TIME
     from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
@@ -31,6 +31,10 @@ def main():
     from pyrenderer_amd.io_utils.read_tungsten import read_file
     scene, cam = read_file(os.path.join(ROOT, "pyrenderer_amd", "media", "cornell-box", "scene.json"))
     flat = flatten_scene(scene)
+    if a.scene == "cubes":
+        from pyrenderer_amd.scenes import instanced_cubes
+        scene, cam = instanced_cubes()
+        flat = flatten_scene(scene)
     if a.scene.startswith("soup:"):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from test_gpu_parity import _soup_scene
