@@ -32,11 +32,19 @@ VALU_PEAK_TFLOPS = 157.3
 # (two child boxes + refs), one triangle record (v0, e1, e2 + id), one light
 # triangle record per shadow query, the per-sample radiance write + its reduction
 # re-read, and the final per-pixel sum write.
-B_NODE, B_TRI, B_LIGHT, B_SAMPLE, B_PIXEL = 64, 48, 64, 24, 12
-# f32 operation accounting (no FMA under the parity contract): slab test of two
-# child boxes ~ 40 ops, Moller-Trumbore ~ 45 ops (with the division).
-F_NODE, F_TRI = 40, 45
+# A node visit reads its child boxes: 64 B for a BVH2 node (2 boxes + refs), 112 B
+# for a BVH4 node (4 boxes SoA + refs); bench picks the figure of the kernel in use.
+B_NODE2, B_NODE4, B_TRI, B_LIGHT, B_SAMPLE, B_PIXEL = 64, 112, 48, 64, 24, 12
+# f32 operation accounting (no FMA under the parity contract): slab test of one
+# child box ~ 20 ops, Moller-Trumbore ~ 45 ops (with the division).
+F_BOX, F_TRI = 20, 45
 
+
+DATA_NOTES = {
+    "cornell": "synthetic (Cornell box scene.json shipped with the reference)",
+    "specular": "synthetic (Cornell box + build-added metal/dielectric boxes and a glass sphere)",
+    "cubes": "synthetic (Cornell box + 83,334 jittered instances of cube.obj, seed 1234)",
+}
 
 # BASELINE.json configs; the bench line is quoted on config 2.
 CONFIGS = {
@@ -180,6 +188,9 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms, launches = ds.kernel_timing()   # HIP events on `stream` around every trace launch
+    # the frame is split into chunks of <= PRT chunk bytes of per-sample radiance (several
+    # trace launches per step at C5); the roofline is per launch
+    launches_per_step = max(launches, 1) / args.steps
     t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -192,10 +203,13 @@ def main():
         # roofline of the dominant kernel (trace_kernel) on rank 0 (per launch)
         per_rank = 1.0 / world
         n_px_rank = len(my_tiles) * T * T
-        bytes_launch = (B_NODE * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank \
-            + B_SAMPLE * n_px_rank * args.spp + B_PIXEL * n_px_rank
+        kinfo = ds.kernel_info()
+        arity = kinfo["bvh_arity"]
+        b_node = B_NODE4 if arity == 4 else B_NODE2
+        bytes_launch = ((b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank
+                        + B_SAMPLE * n_px_rank * args.spp + B_PIXEL * n_px_rank) / launches_per_step
         achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
-        flops_launch = (F_NODE * 2 * nodes + F_TRI * tris) * per_rank
+        flops_launch = (F_BOX * arity * nodes + F_TRI * tris) * per_rank / launches_per_step
         traffic = None
         tj = args.traffic_json
         if tj and os.path.exists(tj):
@@ -212,7 +226,7 @@ def main():
             "metric": "Msamples/sec Cornell box 512²×64spp at 1/2/4/8 GPU; per-pixel L2 vs CPU",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic (Cornell box scene.json)",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": DATA_NOTES[args.scene],
             "config": {"workload": f"{SCENE_NAMES[args.scene]} {W}x{H}, {args.spp} spp, depth {args.depth}",
                        "baseline_config": args.config, "triangles": int(flat.n_tri), "spheres": int(flat.sph.shape[0]),
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
@@ -220,7 +234,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "trace_kernel", "kernel_avg_ms": round(kern_avg_ms, 4),
-                         "bytes_per_launch": int(bytes_launch)},
+                         "bytes_per_launch": int(bytes_launch), "launches_per_step": round(launches_per_step, 3),
+                         "variant": kinfo,
+                         "note": "achieved = logical scene + sample-buffer bytes (DESIGN.md §5); small scenes "
+                                 "are served from LDS, so frac may exceed 1; traffic = PMC HBM bytes per launch"},
             "valu": {"achieved_tflops": round(flops_launch / (kern_avg_ms * 1e-3) / 1e12, 2),
                      "peak_tflops": VALU_PEAK_TFLOPS},
             "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),

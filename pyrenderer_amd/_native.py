@@ -40,6 +40,7 @@ EXPORTS = {
     "prt_bvh_destroy": (None, [_vp]),
     "prt_scene_create": (_i, [_i, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
     "prt_scene_info": (_i, [_vp, _vp]),
+    "prt_scene_kernel": (_i, [_vp, _vp]),
     "prt_scene_destroy": (None, [_vp]),
     "prt_render_tiles": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),

@@ -464,6 +464,18 @@ int prt_scene_info(void* scene, int64_t* info8) {
     return PRT_OK;
 }
 
+int prt_scene_kernel(void* scene, int32_t* out4) {
+    auto* s = (Scene*)scene;
+    if (!s || !out4) return fail(PRT_ERR_ARG, "NULL argument");
+    int var = default_variant(s);
+    bool b4 = prt::variant_uses_bvh4(var);
+    out4[0] = var;
+    out4[1] = b4 ? 4 : 2;
+    out4[2] = prt::variant_uses_lds(var) ? 1 : 0;
+    out4[3] = b4 ? s->stack4 : s->stack;
+    return PRT_OK;
+}
+
 void prt_scene_destroy(void* scene) { destroy_scene((Scene*)scene); }
 
 int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,

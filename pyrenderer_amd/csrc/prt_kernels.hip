@@ -472,10 +472,17 @@ __device__ __forceinline__ void cswap(float& ta, int& ra, float& tb, int& rb) {
     ra = r;
 }
 
-template <bool STATS>
+// MODE 0: per-lane query kind (`any` may differ between lanes); 1: every lane
+// closest-hit; 2: every lane any-hit (phase-aligned shadow iterations).  Any-hit
+// queries need no visiting order, so mode 2 skips the sorting network.
+// Pushes write the slot above the top unconditionally and advance the stack
+// pointer by the hit predicate (no exec-mask branches); the highest slot written
+// is the same as with conditional pushes (<= 3 above the entry top).
+template <bool STATS, int MODE>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                             V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
+                                             V3 d, float tmin, float tmax, bool any_lane, int* lstack, int& hit_id,
                                              float& hit_t, Counters& cn) {
+    const bool any = MODE == 0 ? any_lane : MODE == 2;
     V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     V3 oi = o * inv;
     float best = tmax;
@@ -495,24 +502,31 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
             bool h2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, oi, inv, tmin, best, t2);
             bool h3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, oi, inv, tmin, best, t3);
             int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z), r3 = __float_as_int(rf.w);
-            t0 = h0 ? t0 : INFINITY;
-            t1 = h1 ? t1 : INFINITY;
-            t2 = h2 ? t2 : INFINITY;
-            t3 = h3 ? t3 : INFINITY;
-            int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
-            cswap(t0, r0, t1, r1);
-            cswap(t2, r2, t3, r3);
-            cswap(t0, r0, t2, r2);
-            cswap(t1, r1, t3, r3);
-            cswap(t1, r1, t2, r2);
-            if (nh == 0) {
-                cur = lstack[sp * kBlock];
-                --sp;
+            if (MODE == 2) {
+                lstack[(sp + 1) * kBlock] = r0; sp += h0 ? 1 : 0;
+                lstack[(sp + 1) * kBlock] = r1; sp += h1 ? 1 : 0;
+                lstack[(sp + 1) * kBlock] = r2; sp += h2 ? 1 : 0;
+                int top = lstack[sp * kBlock];
+                cur = h3 ? r3 : top;
+                sp -= h3 ? 0 : 1;
             } else {
-                cur = r0;
-                if (nh > 3) { ++sp; lstack[sp * kBlock] = r3; }
-                if (nh > 2) { ++sp; lstack[sp * kBlock] = r2; }
-                if (nh > 1) { ++sp; lstack[sp * kBlock] = r1; }
+                t0 = h0 ? t0 : INFINITY;
+                t1 = h1 ? t1 : INFINITY;
+                t2 = h2 ? t2 : INFINITY;
+                t3 = h3 ? t3 : INFINITY;
+                int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
+                cswap(t0, r0, t1, r1);
+                cswap(t2, r2, t3, r3);
+                cswap(t0, r0, t2, r2);
+                cswap(t1, r1, t3, r3);
+                cswap(t1, r1, t2, r2);
+                // hit children sorted near-to-far in r0..r(nh-1): visit r0, push the rest far-first
+                lstack[(sp + 1) * kBlock] = r3; sp += nh > 3 ? 1 : 0;
+                lstack[(sp + 1) * kBlock] = r2; sp += nh > 2 ? 1 : 0;
+                lstack[(sp + 1) * kBlock] = r1; sp += nh > 1 ? 1 : 0;
+                int top = lstack[sp * kBlock];
+                cur = nh > 0 ? r0 : top;
+                sp -= nh > 0 ? 0 : 1;
             }
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
@@ -548,6 +562,62 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     hit_id = best_id;
     hit_t = best;
     return best_id >= 0;
+}
+
+// Camera sample of work item `item` (main_taichi.py:89-95): pixel from the tile
+// table, RNG key, jitter, gen_ray.  False when the pixel lies outside the frame.
+// Uniform inputs are laundered through SGPR asm so the compiler cannot hoist
+// their VALU-derived values out of the persistent loop (they would pin VGPRs).
+__device__ __forceinline__ bool camera_sample(const TraceParams& P, uint32_t item, uint32_t chunk_s, uint32_t& st,
+                                              V3& o, V3& d) {
+    int W = P.W, H = P.H, log_tw = P.log_tw, log_tpx = P.log_tpx;
+    float wm1 = P.wm1, hm1 = P.hm1;
+    asm volatile("" : "+s"(W), "+s"(H), "+s"(log_tw), "+s"(log_tpx), "+s"(wm1), "+s"(hm1));
+    uint32_t slot = item - chunk_s * (uint32_t)P.n_slots;
+    uint32_t tk = slot >> log_tpx, loc = slot & ((1u << log_tpx) - 1u);
+    uint32_t xy0 = P.tile_xy[tk];
+    int x = (int)(xy0 >> 16) + (int)(loc & ((1u << log_tw) - 1u));
+    int y = (int)(xy0 & 0xFFFFu) + (int)(loc >> log_tw);
+    if (x >= W || y >= H) return false;
+    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)W + (uint32_t)x, (uint32_t)P.s0 + chunk_s);
+    float r0 = rng_next(st);
+    float u = ((float)x + r0) / wm1;
+    float r1 = rng_next(st);
+    float vv = ((float)y + r1) / hm1;
+    if (P.cam_fast) {
+        // gen_ray for a pinhole affine camera: the same operations minus
+        // those with exactly known results (see TraceParams::cam_fast)
+        float c[12], k[6];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            c[i] = P.cam[i];
+            asm volatile("" : "+s"(c[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            k[i] = P.cam_o[i];
+            k[3 + i] = P.cam_k[i];
+            asm volatile("" : "+s"(k[i]), "+s"(k[3 + i]));
+        }
+        float sd0 = P.cam[16], sd1 = P.cam[17];
+        asm volatile("" : "+s"(sd0), "+s"(sd1));
+        float rx = (u - 0.5f) * sd0 / 0.5f, ry = (vv - 0.5f) * sd1 / 0.5f;
+        float f[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) f[i] = (((rx * c[4 * i] + ry * c[4 * i + 1]) + k[3 + i]) + c[4 * i + 3]) - k[i];
+        float ln = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
+        o = v3(k[0], k[1], k[2]);
+        d = v3(f[0] / ln, f[1] / ln, f[2] / ln);
+    } else {
+        float cam[24];
+#pragma unroll
+        for (int i = 0; i < 20; ++i) {
+            cam[i] = P.cam[i];
+            asm volatile("" : "+s"(cam[i]));
+        }
+        gen_ray(cam, u, vv, st, o, d);
+    }
+    return true;
 }
 
 enum : int { Q_EXT = 0, Q_SHADOW = 1 };
@@ -656,62 +726,14 @@ void trace_kernel(TraceParams P) {
             uint32_t take = need < avail ? need : avail;
             if (((idle >> lane) & 1ull) && rank < take) {
                 item = (int)(q_next + rank);
-                // start a new sample: main_taichi.py:89-95.  Uniform inputs are
-                // laundered through SGPR asm so the compiler cannot hoist their
-                // VALU-derived values out of the loop (they would pin VGPRs).
-                int W = P.W, H = P.H, log_tw = P.log_tw, log_tpx = P.log_tpx;
-                float wm1 = P.wm1, hm1 = P.hm1;
-                asm volatile("" : "+s"(W), "+s"(H), "+s"(log_tw), "+s"(log_tpx), "+s"(wm1), "+s"(hm1));
-                uint32_t slot = (uint32_t)item - chunk_s * (uint32_t)P.n_slots;
-                uint32_t tk = slot >> log_tpx, loc = slot & ((1u << log_tpx) - 1u);
-                uint32_t xy0 = P.tile_xy[tk];
-                int x = (int)(xy0 >> 16) + (int)(loc & ((1u << log_tw) - 1u));
-                int y = (int)(xy0 & 0xFFFFu) + (int)(loc >> log_tw);
+                // start a new sample: main_taichi.py:89-95
                 L = v3(0, 0, 0);
-                if (x >= W || y >= H) {
+                bool ok = camera_sample(P, (uint32_t)item, chunk_s, st, o, d);
+                if (!ok) {
                     float* out = P.out + (size_t)item * 3;
                     out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
                     item = -2;  // served, nothing to trace this iteration
                 } else {
-                    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)W + (uint32_t)x, (uint32_t)P.s0 + chunk_s);
-                    float r0 = rng_next(st);
-                    float u = ((float)x + r0) / wm1;
-                    float r1 = rng_next(st);
-                    float vv = ((float)y + r1) / hm1;
-                    if (P.cam_fast) {
-                        // gen_ray for a pinhole affine camera: the same operations minus
-                        // those with exactly known results (see TraceParams::cam_fast)
-                        float c[12], k[6];
-#pragma unroll
-                        for (int i = 0; i < 12; ++i) {
-                            c[i] = P.cam[i];
-                            asm volatile("" : "+s"(c[i]));
-                        }
-#pragma unroll
-                        for (int i = 0; i < 3; ++i) {
-                            k[i] = P.cam_o[i];
-                            k[3 + i] = P.cam_k[i];
-                            asm volatile("" : "+s"(k[i]), "+s"(k[3 + i]));
-                        }
-                        float sd0 = P.cam[16], sd1 = P.cam[17];
-                        asm volatile("" : "+s"(sd0), "+s"(sd1));
-                        float rx = (u - 0.5f) * sd0 / 0.5f, ry = (vv - 0.5f) * sd1 / 0.5f;
-                        float f[3];
-#pragma unroll
-                        for (int i = 0; i < 3; ++i)
-                            f[i] = (((rx * c[4 * i] + ry * c[4 * i + 1]) + k[3 + i]) + c[4 * i + 3]) - k[i];
-                        float ln = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
-                        o = v3(k[0], k[1], k[2]);
-                        d = v3(f[0] / ln, f[1] / ln, f[2] / ln);
-                    } else {
-                        float cam[24];
-#pragma unroll
-                        for (int i = 0; i < 20; ++i) {
-                            cam[i] = P.cam[i];
-                            asm volatile("" : "+s"(cam[i]));
-                        }
-                        gen_ray(cam, u, vv, st, o, d);
-                    }
                     beta = v3(1, 1, 1);
                     bounce = 0;
                     qtype = Q_EXT;
@@ -748,14 +770,17 @@ void trace_kernel(TraceParams P) {
             hit = traverse_u<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         } else if (TRAV == 2) {
             hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+        } else if (TRAV == 3 && PHASE) {
+            if (do_shadow) hit = traverse_ww4<STATS, 2>(g_nodes, g_tris, o, d, kTMin, tmax, true, lstack, hid, ht, cn);
+            else hit = traverse_ww4<STATS, 1>(g_nodes, g_tris, o, d, kTMin, tmax, false, lstack, hid, ht, cn);
         } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         } else {
             park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
             park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
             park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
             asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
             asm volatile("" ::: "memory");
             float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
             beta = v3(k0.x, k0.y, k0.z);
@@ -976,7 +1001,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
 
 }  // namespace
 
-// variant table: (traversal | 8 if phase-aligned, LDS scene, min waves per SIMD); see prt_kernels.h
+// variant table: (traversal | 8 phase-aligned, LDS scene, min waves per SIMD); see prt_kernels.h
 #define PRT_VARIANTS(X)                                   \
     X(kVarSplit, 0, false, 1)                             \
     X(kVarUnified, 1, false, 1)                           \
