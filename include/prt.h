@@ -40,6 +40,7 @@ extern "C" {
 /* render flags */
 #define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
 #define PRT_FLAG_TIME 0x2u   /* time the trace kernel with HIP events on its stream */
+#define PRT_FLAG_NO_PRIMARY_KERNEL 0x4u /* generate camera rays inside the trace kernel (A/B; same image) */
 /* trace-kernel variant in bits 8..15 (0 = automatic; the numbering is the
  * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: split / unified / while-while
  * traversal, BVH2 / BVH4, global / LDS-resident scene, occupancy targets,

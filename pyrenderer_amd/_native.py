@@ -13,6 +13,7 @@ from .build import LIB
 PRT_OK = 0
 PRT_FLAG_STATS = 0x1
 PRT_FLAG_TIME = 0x2
+PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int

@@ -94,6 +94,7 @@ struct Scene {
     int n_lt = 0;                    // emitter triangles
     int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
+    DevBuf rays;                     // primary rays of one launch (camera_kernel)
     DevBuf nodes, nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
     int64_t n_node4_f4 = 0;
     int32_t depth4 = 0;
@@ -124,7 +125,7 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
+    for (DevBuf* b : {&s->rays, &s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
                       &s->tiles, &s->buf, &s->acc, &s->work, &s->stats})
         b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
@@ -180,6 +181,14 @@ int default_variant(const Scene* s) {
     return smem * 6 <= 160 * 1024 ? prt::kVarWW4PhLds6 : prt::kVarWW4Lds;
 }
 
+// Pinhole camera with an affine matrix (no aperture, last row (0,0,0,1), all finite):
+// the kernels may use the exact gen_ray shortcut (TraceParams::cam_fast).
+bool camera_is_fast(const float* cam) {
+    bool fin = true;
+    for (int i = 0; i < 20; ++i) fin = fin && std::isfinite(cam[i]);
+    return fin && !(cam[19] > 0.0f) && cam[12] == 0.0f && cam[13] == 0.0f && cam[14] == 0.0f && cam[15] == 1.0f;
+}
+
 // Enqueue the whole render of a tile set on `stream`, result in d_acc.
 int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,
                    int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc, hipStream_t stream) {
@@ -197,11 +206,16 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
         HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots, stream));
         return PRT_OK;
     }
+    // per-sample buffers: radiance (12 B) + primary ray (16 B, pinhole cameras)
+    const bool cam_fast = camera_is_fast(cam);
+    const bool primary = cam_fast && !(flags & PRT_FLAG_NO_PRIMARY_KERNEL);
     int64_t per_sample = n_slots * 3 * (int64_t)sizeof(float);
-    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)s->chunk_bytes / per_sample));
+    int64_t per_sample_all = per_sample + (primary ? n_slots * 16 : 0);
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)s->chunk_bytes / per_sample_all));
     // keep every chunk's item count below 2^31 (32-bit work counter)
     chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, ((int64_t)1 << 31) / n_slots - 1));
     HIP_TRY(s->buf.ensure((size_t)(chunk * per_sample)));
+    if (primary) HIP_TRY(s->rays.ensure((size_t)(chunk * n_slots * 16)));
     const bool stats = (flags & PRT_FLAG_STATS) != 0;
     const bool timed = (flags & PRT_FLAG_TIME) != 0;
     if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), stream));
@@ -219,10 +233,8 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.dl_r = s->direct_rgb[0]; P.dl_g = s->direct_rgb[1]; P.dl_b = s->direct_rgb[2];
     std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
     {
-        bool fin = true;
-        for (int i = 0; i < 20; ++i) fin = fin && std::isfinite(cam[i]);
-        P.cam_fast = fin && !(cam[19] > 0.0f) && cam[12] == 0.0f && cam[13] == 0.0f && cam[14] == 0.0f &&
-                     cam[15] == 1.0f;
+        P.cam_fast = cam_fast ? 1 : 0;
+        P.rays = primary ? (const float4*)s->rays.p : nullptr;
         const float rd2 = -cam[18];
         for (int i = 0; i < 3; ++i) {
             const float* c = cam + 4 * i;
@@ -279,6 +291,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
         HIP_TRY(hipMemsetAsync(s->work.p, 0, 16, stream));
+        if (primary) HIP_TRY(prt::launch_camera(P, (float4*)s->rays.p, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
         HIP_TRY(prt::launch_trace(P, stack, var, grid, stats, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k + 1], stream));

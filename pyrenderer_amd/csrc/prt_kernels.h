@@ -21,6 +21,7 @@ struct TraceParams {
     // the ray origin M (0,0,0,1) and the constant terms rd.z * M[i][2] of gen_ray,
     // evaluated on the host in the kernel's f32 order (camera_taichi.py:47-74)
     int cam_fast;
+    const float4* rays;       // primary rays of this launch from camera_kernel, or null (generated in the refill)
     float cam_o[3], cam_k[3];
     int W, H;                 // full frame (u = (x + r) / (W - 1))
     float wm1, hm1;           // (float)(W - 1), (float)(H - 1)
@@ -67,6 +68,7 @@ bool variant_uses_bvh4(int var);
 
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);
+hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream);
 size_t lds_scene_bytes(const TraceParams& P);  // LDS-resident scene + shading data
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);

@@ -564,21 +564,27 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     return best_id >= 0;
 }
 
-// Camera sample of work item `item` (main_taichi.py:89-95): pixel from the tile
-// table, RNG key, jitter, gen_ray.  False when the pixel lies outside the frame.
-// Uniform inputs are laundered through SGPR asm so the compiler cannot hoist
-// their VALU-derived values out of the persistent loop (they would pin VGPRs).
-__device__ __forceinline__ bool camera_sample(const TraceParams& P, uint32_t item, uint32_t chunk_s, uint32_t& st,
-                                              V3& o, V3& d) {
-    int W = P.W, H = P.H, log_tw = P.log_tw, log_tpx = P.log_tpx;
-    float wm1 = P.wm1, hm1 = P.hm1;
-    asm volatile("" : "+s"(W), "+s"(H), "+s"(log_tw), "+s"(log_tpx), "+s"(wm1), "+s"(hm1));
+// Pixel of work item `item` (slot = tile-major, row, column); xy0 = the item's
+// tile origin (x0 << 16 | y0).  Uniform inputs are laundered through SGPR asm so
+// the compiler cannot hoist their VALU-derived values out of the persistent loop
+// (they would pin VGPRs).
+__device__ __forceinline__ void pixel_of(const TraceParams& P, uint32_t item, uint32_t chunk_s, uint32_t xy0, int& x,
+                                         int& y) {
+    int log_tw = P.log_tw, log_tpx = P.log_tpx;
+    asm volatile("" : "+s"(log_tw), "+s"(log_tpx));
     uint32_t slot = item - chunk_s * (uint32_t)P.n_slots;
-    uint32_t tk = slot >> log_tpx, loc = slot & ((1u << log_tpx) - 1u);
-    uint32_t xy0 = P.tile_xy[tk];
-    int x = (int)(xy0 >> 16) + (int)(loc & ((1u << log_tw) - 1u));
-    int y = (int)(xy0 & 0xFFFFu) + (int)(loc >> log_tw);
-    if (x >= W || y >= H) return false;
+    uint32_t loc = slot & ((1u << log_tpx) - 1u);
+    x = (int)(xy0 >> 16) + (int)(loc & ((1u << log_tw) - 1u));
+    y = (int)(xy0 & 0xFFFFu) + (int)(loc >> log_tw);
+}
+
+// Camera sample for pixel (x, y) of sample `chunk_s` (main_taichi.py:89-95): RNG key,
+// jitter, gen_ray.
+__device__ __forceinline__ void camera_ray(const TraceParams& P, int x, int y, uint32_t chunk_s, uint32_t& st, V3& o,
+                                           V3& d) {
+    int W = P.W;
+    float wm1 = P.wm1, hm1 = P.hm1;
+    asm volatile("" : "+s"(W), "+s"(wm1), "+s"(hm1));
     st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)W + (uint32_t)x, (uint32_t)P.s0 + chunk_s);
     float r0 = rng_next(st);
     float u = ((float)x + r0) / wm1;
@@ -617,7 +623,25 @@ __device__ __forceinline__ bool camera_sample(const TraceParams& P, uint32_t ite
         }
         gen_ray(cam, u, vv, st, o, d);
     }
-    return true;
+}
+
+// Primary rays of one launch, generated with every lane busy (the persistent
+// trace kernel would otherwise run this code with the few lanes it refills):
+// rays[item] = (d, rng state after the camera draws).  Pinhole cameras only
+// (TraceParams::cam_fast), whose origin is the uniform cam_o.
+__global__ __launch_bounds__(kBlock) void camera_kernel(TraceParams P, float4* __restrict__ rays) {
+    uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (item >= P.n_items) return;
+    uint32_t cs = (uint32_t)(item / (uint64_t)P.n_slots);
+    uint32_t slot = (uint32_t)item - cs * (uint32_t)P.n_slots;
+    uint32_t xy0 = P.tile_xy[slot >> P.log_tpx];
+    int x, y;
+    pixel_of(P, (uint32_t)item, cs, xy0, x, y);
+    if (x >= P.W || y >= P.H) return;
+    uint32_t st;
+    V3 o, d;
+    camera_ray(P, x, y, cs, st, o, d);
+    rays[item] = make_float4(d.x, d.y, d.z, __uint_as_float(st));
 }
 
 enum : int { Q_EXT = 0, Q_SHADOW = 1 };
@@ -685,6 +709,7 @@ void trace_kernel(TraceParams P) {
     Counters cn = {0, 0, 0, 0, 0, 0};
     uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
     uint32_t chunk_s = 0;   // wave-uniform: sample index (within the launch) of the current chunk
+    uint32_t chunk_xy0 = 0; // wave-uniform: origin of the current chunk's tile
 
     // diagnostic (STATS) wave-level clocks: refill / traversal / shading, iterations, active lanes
     uint64_t c_refill = 0, c_trav = 0, c_shade = 0, n_iter = 0, n_active = 0;
@@ -717,6 +742,9 @@ void trace_kernel(TraceParams P) {
                     // n_slots is a multiple of 64 (tile sizes are powers of two >= 64 px),
                     // so a chunk never straddles two samples: one scalar division per chunk
                     chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
+                    // tiles hold >= 64 pixels (powers of two), so the chunk lies in one tile
+                    uint32_t tk = (base - chunk_s * (uint32_t)P.n_slots) >> P.log_tpx;
+                    chunk_xy0 = __builtin_amdgcn_readfirstlane(P.tile_xy[tk]);
                 }
                 avail = q_end - q_next;
             }
@@ -728,7 +756,23 @@ void trace_kernel(TraceParams P) {
                 item = (int)(q_next + rank);
                 // start a new sample: main_taichi.py:89-95
                 L = v3(0, 0, 0);
-                bool ok = camera_sample(P, (uint32_t)item, chunk_s, st, o, d);
+                int x, y;
+                pixel_of(P, (uint32_t)item, chunk_s, chunk_xy0, x, y);
+                int W = P.W, H = P.H;
+                asm volatile("" : "+s"(W), "+s"(H));
+                bool ok = x < W && y < H;
+                if (ok) {
+                    if (P.rays) {
+                        float4 r = P.rays[item];
+                        d = v3(r.x, r.y, r.z);
+                        st = __float_as_uint(r.w);
+                        float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
+                        asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
+                        o = v3(o0, o1, o2);
+                    } else {
+                        camera_ray(P, x, y, chunk_s, st, o, d);
+                    }
+                }
                 if (!ok) {
                     float* out = P.out + (size_t)item * 3;
                     out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
@@ -757,11 +801,16 @@ void trace_kernel(TraceParams P) {
         bool hit;
         if (STATS) {
             if (qtype == Q_EXT) cn.ext++; else cn.shadow++;
+            // wave-level clocks: the first active lane books the interval
+            const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
+            const uint64_t active = __ballot(true);
             t_b = __builtin_amdgcn_s_memtime();
-            c_refill += t_b - t_a;
+            if (leader) {
+                c_refill += t_b - t_a;
+                n_iter++;
+                n_active += (uint64_t)__popcll(active);
+            }
             t_a = t_b;
-            n_iter++;
-            n_active += (uint64_t)__popcll(__ballot(true));
         }
         if (TRAV == 0) {
             if (qtype == Q_EXT) hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
@@ -804,16 +853,18 @@ void trace_kernel(TraceParams P) {
             ht = best;
         }
         if (STATS) {
+            const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
             t_b = __builtin_amdgcn_s_memtime();
-            c_trav += t_b - t_a;
+            if (leader) c_trav += t_b - t_a;
             t_a = t_b;
-            // wave-level loop trips = max over lanes; lane-level = sum
+            // wave-level loop trips = max over the participating lanes; lane-level = sum
             uint32_t mi = cn.it_inner, ml = cn.it_leaf;
             for (int off = 32; off > 0; off >>= 1) {
                 mi = max(mi, (uint32_t)__shfl_xor((int)mi, off));
                 ml = max(ml, (uint32_t)__shfl_xor((int)ml, off));
             }
-            w_inner += mi; w_leaf += ml; l_inner += cn.it_inner; l_leaf += cn.it_leaf;
+            if (leader) { w_inner += mi; w_leaf += ml; }
+            l_inner += cn.it_inner; l_leaf += cn.it_leaf;
             cn.it_inner = 0; cn.it_leaf = 0;
         }
         // ------------------------------------------------- shade the result
@@ -952,7 +1003,10 @@ void trace_kernel(TraceParams P) {
             out[0] = L.x; out[1] = L.y; out[2] = L.z;
             item = -1;
         }
-        if (STATS) c_shade += __builtin_amdgcn_s_memtime() - t_a;
+        if (STATS) {
+            const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
+            if (leader) c_shade += __builtin_amdgcn_s_memtime() - t_a;
+        }
     }
     if (STATS) {
         uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
@@ -960,18 +1014,15 @@ void trace_kernel(TraceParams P) {
             a += __shfl_down(a, off); b += __shfl_down(b, off);
             c += __shfl_down(c, off); e += __shfl_down(e, off);
         }
+        uint64_t wv[7] = {c_refill, c_trav, c_shade, n_iter, n_active, w_inner, w_leaf};
+        for (int k = 0; k < 7; ++k)
+            for (int off = 32; off > 0; off >>= 1) wv[k] += __shfl_down(wv[k], off);
         if (lane == 0) {
             atomicAdd(P.stats + 0, (unsigned long long)a);
             atomicAdd(P.stats + 1, (unsigned long long)b);
             atomicAdd(P.stats + 2, (unsigned long long)c);
             atomicAdd(P.stats + 3, (unsigned long long)e);
-            atomicAdd(P.stats + 4, (unsigned long long)c_refill);
-            atomicAdd(P.stats + 5, (unsigned long long)c_trav);
-            atomicAdd(P.stats + 6, (unsigned long long)c_shade);
-            atomicAdd(P.stats + 7, (unsigned long long)n_iter);
-            atomicAdd(P.stats + 8, (unsigned long long)n_active);
-            atomicAdd(P.stats + 9, (unsigned long long)w_inner);
-            atomicAdd(P.stats + 10, (unsigned long long)w_leaf);
+            for (int k = 0; k < 7; ++k) atomicAdd(P.stats + 4 + k, (unsigned long long)wv[k]);
         }
         {
             uint64_t a2 = l_inner, b2 = l_leaf;
@@ -1073,6 +1124,12 @@ hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool
         case 32: return launch_stack<32>(P, var, grid, stats, smem, stream);
         default: return launch_stack<64>(P, var, grid, stats, smem, stream);
     }
+}
+
+hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream) {
+    int64_t grid = ((int64_t)P.n_items + kBlock - 1) / kBlock;
+    camera_kernel<<<(unsigned)grid, kBlock, 0, stream>>>(P, rays);
+    return hipGetLastError();
 }
 
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream) {

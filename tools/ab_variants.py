@@ -16,13 +16,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def vflags(v):
+    """'15' -> variant 15; '15np' -> variant 15 with camera rays generated inside the trace kernel."""
+    from pyrenderer_amd._native import PRT_FLAG_NO_PRIMARY_KERNEL
+    np_ = v.endswith("np")
+    return (int(v[:-2] if np_ else v) << 8) | (PRT_FLAG_NO_PRIMARY_KERNEL if np_ else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", type=int, nargs="+", default=[1, 2, 3])
+    ap.add_argument("--variants", nargs="+", default=["1", "2", "3"],
+                    help="kernel variant numbers; suffix 'np' = camera rays inside the trace kernel")
     ap.add_argument("--scene", default="cornell", help="cornell | cubes | soup:N (random triangle soup of N tris in the box)")
     a = ap.parse_args()
     from pyrenderer_amd._native import PRT_FLAG_TIME
@@ -47,7 +55,7 @@ def main():
     ref = None
     for r in range(a.rounds + 1):
         for v in a.variants:
-            flags = PRT_FLAG_TIME | (v << 8)
+            flags = PRT_FLAG_TIME | vflags(v)
             t0 = time.perf_counter()
             out, _ = ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, flags)
             wall = time.perf_counter() - t0
@@ -60,7 +68,7 @@ def main():
     samples = W * H * a.spp
     from pyrenderer_amd._native import PRT_FLAG_STATS
     for v in a.variants:
-        ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, PRT_FLAG_STATS | (v << 8))
+        ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, PRT_FLAG_STATS | vflags(v))
         dg = ds.diag_stats().astype(np.float64)
         tot = dg[4] + dg[5] + dg[6]
         print(json.dumps({"variant": v, "diag": {"refill_frac": round(dg[4] / tot, 3), "trav_frac": round(dg[5] / tot, 3),
@@ -75,7 +83,9 @@ def main():
               flush=True)
     for v, rows in res.items():
         ms = np.array([x[0] for x in rows])
+        wall = np.array([x[1] for x in rows])
         print(json.dumps({"variant": v, "kernel_ms_median": round(float(np.median(ms)), 3),
+                          "wall_ms_median": round(float(np.median(wall)), 3),
                           "kernel_ms_min": round(float(ms.min()), 3),
                           "msamples_s": round(samples / np.median(ms) / 1e3, 1),
                           "identical_to_first": all(x[2] for x in rows), "scene": a.scene,
