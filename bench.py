@@ -34,7 +34,8 @@ VALU_PEAK_TFLOPS = 157.3
 # re-read, and the final per-pixel sum write.
 # A node visit reads its child boxes: 64 B for a BVH2 node (2 boxes + refs), 112 B
 # for a BVH4 node (4 boxes SoA + refs); bench picks the figure of the kernel in use.
-B_NODE2, B_NODE4, B_TRI, B_LIGHT, B_SAMPLE, B_PIXEL = 64, 112, 48, 64, 24, 12
+# (64 B for a quantised BVH4 node, the layout used for scenes that do not fit LDS).
+B_NODE2, B_NODE4, B_NODE4Q, B_TRI, B_LIGHT, B_SAMPLE, B_PIXEL = 64, 112, 64, 48, 64, 24, 12
 # f32 operation accounting (no FMA under the parity contract): slab test of one
 # child box ~ 20 ops, Moller-Trumbore ~ 45 ops (with the division).
 F_BOX, F_TRI = 20, 45
@@ -205,7 +206,7 @@ def main():
         n_px_rank = len(my_tiles) * T * T
         kinfo = ds.kernel_info()
         arity = kinfo["bvh_arity"]
-        b_node = B_NODE4 if arity == 4 else B_NODE2
+        b_node = (B_NODE4Q if kinfo["quantized"] else B_NODE4) if arity == 4 else B_NODE2
         bytes_launch = ((b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank
                         + B_SAMPLE * n_px_rank * args.spp + B_PIXEL * n_px_rank) / launches_per_step
         achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9

@@ -127,7 +127,8 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
  * total ms and number of trace launches. */
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
 /* trace-kernel variant chosen for this scene when flags select none:
- * out4 = {variant, BVH arity (2 or 4), scene LDS-resident (0/1), traversal stack entries} */
+ * out4 = {variant, BVH arity (2 or 4), bit 0 scene LDS-resident | bit 1 quantised nodes,
+ *         LDS traversal stack entries per lane} */
 int prt_scene_kernel(void* scene, int32_t* out4);
 /* counters of the last render call made with PRT_FLAG_STATS (synchronises) */
 int prt_last_stats(void* scene, uint64_t* stats4);

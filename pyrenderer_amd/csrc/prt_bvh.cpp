@@ -349,4 +349,56 @@ void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
     out->stack_need = 3 * (out->depth + 1) + 1;
 }
 
+void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out) {
+    out->assign((size_t)b4.n_nodes * 16, 0.0f);
+    const double margin = 2.0 * (double)pad;
+    for (int64_t n = 0; n < b4.n_nodes; ++n) {
+        const float* f = b4.nodes.data() + (size_t)n * 32;
+        float* q = out->data() + (size_t)n * 16;
+        int32_t refs[4];
+        std::memcpy(refs, f + 24, 16);
+        bool ok[4];
+        for (int k = 0; k < 4; ++k) ok[k] = std::isfinite(f[k]);   // empty slots hold +inf
+        float origin[3], step[3];
+        uint32_t ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0};
+        for (int a = 0; a < 3; ++a) {
+            double lo = INFINITY, hi = -INFINITY;
+            for (int k = 0; k < 4; ++k)
+                if (ok[k]) {
+                    lo = std::min(lo, (double)f[(2 * a) * 4 + k]);
+                    hi = std::max(hi, (double)f[(2 * a + 1) * 4 + k]);
+                }
+            if (!(lo <= hi)) { lo = 0.0; hi = 0.0; }
+            // origin rounded down to f32; grid step = the f32 at or above range / 254
+            float o = (float)(lo - margin);
+            if ((double)o > lo - margin) o = std::nextafter(o, -INFINITY);
+            double ext = hi + margin - (double)o;
+            float stf = (float)std::max(ext / 254.0, 1e-30);
+            if ((double)stf < ext / 254.0) stf = std::nextafter(stf, INFINITY);
+            double st = (double)stf;
+            origin[a] = o;
+            step[a] = (float)st;
+            for (int k = 0; k < 4; ++k) {
+                if (!ok[k]) continue;
+                double l = (double)f[(2 * a) * 4 + k], h = (double)f[(2 * a + 1) * 4 + k];
+                long ql_k = (long)std::floor((l - margin - (double)o) / st);
+                long qh_k = (long)std::ceil((h + margin - (double)o) / st);
+                ql_k = std::max(0L, std::min(255L, ql_k));
+                qh_k = std::max(0L, std::min(255L, qh_k));
+                ql[a] |= (uint32_t)ql_k << (8 * k);
+                qh[a] |= (uint32_t)qh_k << (8 * k);
+            }
+        }
+        q[0] = origin[0]; q[1] = origin[1]; q[2] = origin[2]; q[3] = step[0];
+        q[4] = step[1]; q[5] = step[2];
+        std::memcpy(q + 6, &ql[0], 4); std::memcpy(q + 7, &qh[0], 4);
+        std::memcpy(q + 8, &ql[1], 4); std::memcpy(q + 9, &qh[1], 4);
+        std::memcpy(q + 10, &ql[2], 4); std::memcpy(q + 11, &qh[2], 4);
+        for (int k = 0; k < 4; ++k) {
+            int32_t r = ok[k] ? refs[k] : 0x7FFFFFFF;
+            std::memcpy(q + 12 + k, &r, 4);
+        }
+    }
+}
+
 }  // namespace prt

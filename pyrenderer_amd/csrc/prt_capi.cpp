@@ -95,10 +95,15 @@ struct Scene {
     int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
     DevBuf rays;                     // primary rays of one launch (camera_kernel)
+    DevBuf nodes4q;                  // quantised BVH4 (prt_internal.h)
+    int64_t n_node4q_f4 = 0;
     DevBuf nodes, nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
     int64_t n_node4_f4 = 0;
     int32_t depth4 = 0;
     int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
+    int need4 = 0;                   // worst-case BVH4 traversal stack entries
+    int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
+    DevBuf spill;                    // spill variants: deep stack entries
     int64_t n_sph = 0;
     DevBuf tiles, buf, acc, work, stats;
     hipStream_t stream = nullptr;
@@ -125,7 +130,7 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->rays, &s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
+    for (DevBuf* b : {&s->rays, &s->nodes4q, &s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
                       &s->tiles, &s->buf, &s->acc, &s->work, &s->stats})
         b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
@@ -172,8 +177,8 @@ bool lds_fits4(const Scene* s) { return lds_fits_var(s, true); }
 // LDS-resident scene when it fits; the >= 6 waves/SIMD build when six blocks' LDS
 // still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
 int default_variant(const Scene* s) {
+    if (!lds_fits4(s)) return prt::kVarWW4QSp5;  // global scene: 64-B quantised nodes, 16-entry LDS stack + spill
     if (!s->stack4) return prt::kVarWW;
-    if (!lds_fits4(s)) return prt::kVarWW4;
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
     scene_sizes(s, true, P);
@@ -262,16 +267,27 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     if (var == 0) var = default_variant(s);
     if (var < prt::kVarSplit || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
     const bool b4 = prt::variant_uses_bvh4(var);
+    const bool spill = prt::variant_spills(var);
     if (b4) {
-        if (s->stack4 == 0) return fail(PRT_ERR_ARG, "BVH4 too deep for the traversal stack variants");
+        if (s->stack4 == 0 && !spill) return fail(PRT_ERR_ARG, "BVH4 too deep for the traversal stack variants");
         P.nodes = (const float4*)s->nodes4.p;
         P.n_node_f4 = (int)s->n_node4_f4;
-        stack = s->stack4;
+        stack = spill ? s->spill_lds : s->stack4;
+        if (prt::variant_quantized(var)) {
+            P.nodes = (const float4*)s->nodes4q.p;
+            P.n_node_f4 = (int)s->n_node4q_f4;
+        }
     }
     if (prt::variant_uses_lds(var) && !(b4 ? lds_fits4(s) : lds_fits(s)))
         return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
     int& occ = s->occ[2 * var + (stats ? 1 : 0)];
     if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(stack, var, stats, prt::trace_smem_bytes(stack, var, P)));
+    if (spill) {
+        // entries [spill_lds, need4] of every lane of the largest grid, plus one slot of headroom
+        size_t per_lane = (size_t)std::max(1, s->need4 + 2 - s->spill_lds);
+        HIP_TRY(s->spill.ensure(per_lane * (size_t)occ * s->cus * 256 * sizeof(int)));
+        P.spill = (int*)s->spill.p;
+    }
 
     int64_t n_chunks = (spp + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
@@ -433,7 +449,12 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             s->depth4 = b4.depth;
             s->n_node4_f4 = (int64_t)b4.nodes.size() / 4;
             s->stack4 = b4.stack_need <= 64 ? prt::stack_variant(b4.stack_need - 1) : 0;
+            s->need4 = b4.stack_need;
             if ((rc = upload(s->nodes4, b4.nodes.data(), sizeof(float) * b4.nodes.size(), &s->device_bytes))) break;
+            std::vector<float> q4;
+            prt::quantize_bvh4(b4, bvh.pad, &q4);
+            s->n_node4q_f4 = (int64_t)q4.size() / 4;
+            if ((rc = upload(s->nodes4q, q4.data(), sizeof(float) * q4.size(), &s->device_bytes))) break;
         }
         if ((rc = upload(s->tris, bvh.tris.data(), sizeof(float) * bvh.tris.size(), &s->device_bytes))) break;
         if ((rc = upload(s->tri_nm, nm.data(), sizeof(float) * nm.size(), &s->device_bytes))) break;
@@ -453,13 +474,17 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         s->cus = prop.multiProcessorCount;
         s->n_node_f4 = (int64_t)bvh.nodes.size() / 4;
         s->n_tri_f4 = (int64_t)bvh.tris.size() / 4;
+        if (const char* sl = std::getenv("PRT_SPILL_LDS")) {
+            int v = std::atoi(sl);
+            s->spill_lds = v == 4 ? 4 : v == 32 ? 32 : 16;
+        }
         {
             prt::TraceParams Q;
             std::memset(&Q, 0, sizeof(Q));
             int var = default_variant(s);
             bool b4 = prt::variant_uses_bvh4(var);
             scene_sizes(s, b4, Q);
-            int stk = b4 ? s->stack4 : s->stack;
+            int stk = prt::variant_spills(var) ? s->spill_lds : b4 ? s->stack4 : s->stack;
             s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(stk, var, false, prt::trace_smem_bytes(stk, var, Q)));
         }
         if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
@@ -484,8 +509,8 @@ int prt_scene_kernel(void* scene, int32_t* out4) {
     bool b4 = prt::variant_uses_bvh4(var);
     out4[0] = var;
     out4[1] = b4 ? 4 : 2;
-    out4[2] = prt::variant_uses_lds(var) ? 1 : 0;
-    out4[3] = b4 ? s->stack4 : s->stack;
+    out4[2] = (prt::variant_uses_lds(var) ? 1 : 0) | (prt::variant_quantized(var) ? 2 : 0);
+    out4[3] = prt::variant_spills(var) ? s->spill_lds : b4 ? s->stack4 : s->stack;
     return PRT_OK;
 }
 

@@ -48,6 +48,17 @@ struct Bvh4Host {
 };
 void collapse_bvh4(const BvhHost& b2, Bvh4Host* out);
 
+// Quantised BVH4 for scenes read from HBM: one node = 4 x float4 = 64 B (two per
+// 128-B cache line, half the BVH4 footprint):
+//   f[0] = (origin.x, origin.y, origin.z, s.x)    s = grid step per axis (range / 254, rounded up)
+//   f[1] = (s.y, s.z, qlo.x[4], qhi.x[4])         q = u8 per child packed in a u32
+//   f[2] = (qlo.y[4], qhi.y[4], qlo.z[4], qhi.z[4])
+//   f[3] = child refs (as Bvh4Host), empty slots = 0x7FFFFFFF (masked by the kernel)
+// Child box = origin + q * s, rounded outward so that it contains the float box
+// with at least `pad` to spare on every side (conservative: traversal unchanged).
+constexpr int kNodeQF4 = 4;
+void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out);
+
 // Builds a binned-SAH BVH2 over triangles (tri_v: n x 9 f32 world vertices).
 // Box padding keeps the slab test conservative w.r.t. Moller-Trumbore's own
 // rounding so traversal returns exactly the brute-force closest hit.

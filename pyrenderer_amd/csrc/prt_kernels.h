@@ -21,6 +21,7 @@ struct TraceParams {
     // the ray origin M (0,0,0,1) and the constant terms rd.z * M[i][2] of gen_ray,
     // evaluated on the host in the kernel's f32 order (camera_taichi.py:47-74)
     int cam_fast;
+    int* spill;               // spill variants: per-lane stack entries beyond the LDS part (stride = grid threads)
     const float4* rays;       // primary rays of this launch from camera_kernel, or null (generated in the refill)
     float cam_o[3], cam_k[3];
     int W, H;                 // full frame (u = (x + r) / (W - 1))
@@ -62,8 +63,17 @@ constexpr int kVarWW4PhLds6 = 15;   // BVH4, LDS scene, >= 6 waves, phase-aligne
 constexpr int kVarWW4PhLds = 16;    // ... LDS scene, no occupancy target
 constexpr int kVarWW4Ph = 17;       // ... global scene
 constexpr int kVarWW4Ph5 = 18;      // ... global scene, >= 5 waves
-constexpr int kVarLast = 18;
+constexpr int kVarWW4Sp = 19;       // BVH4, global scene, 32-entry LDS stack + global spill area
+constexpr int kVarWW4Sp4 = 20;      // ... >= 4 waves per SIMD
+constexpr int kVarWW4Sp5 = 21;      // ... >= 5 waves per SIMD
+constexpr int kVarWW4QSp = 22;      // quantised 64-B BVH4 nodes, spill stack, global scene
+constexpr int kVarWW4QSp5 = 23;     // ... >= 5 waves per SIMD
+constexpr int kVarWW4QPhSp = 24;    // ... phase-aligned
+constexpr int kVarWW4QSp6 = 25;     // ... >= 6 waves per SIMD
+constexpr int kVarLast = 25;
 bool variant_uses_lds(int var);
+bool variant_spills(int var);
+bool variant_quantized(int var);
 bool variant_uses_bvh4(int var);
 
 int stack_variant(int bvh_depth);

@@ -17,6 +17,7 @@
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "prt_kernels.h"
@@ -203,7 +204,7 @@ __device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, f
 }
 
 // ---------------------------------------------------------------- traversal
-struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf; };
+struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp; };
 
 // Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
 __device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 oi, V3 inv,
@@ -472,41 +473,105 @@ __device__ __forceinline__ void cswap(float& ta, int& ra, float& tb, int& rb) {
     ra = r;
 }
 
+// Per-lane traversal stacks.  LdsStack: entry k at l[k * kBlock] (conflict-free).
+// SpillStack: the first LST entries in LDS, deeper ones in a per-lane global area
+// (stride = all threads of the grid); deep stacks are rare (max 24 entries measured on
+// the 1 M-triangle scene against a worst-case bound of 46), so a small LDS stack keeps
+// occupancy and the spill branch is almost never taken.
+struct LdsStack {
+    int* l;
+    __device__ __forceinline__ void put(int k, int v) { l[k * kBlock] = v; }
+    __device__ __forceinline__ int get(int k) const { return l[k * kBlock]; }
+};
+template <int LST>
+struct SpillStack {
+    int* l;
+    int* g;
+    uint32_t gs;
+    __device__ __forceinline__ void put(int k, int v) {
+        if (k < LST) l[k * kBlock] = v;
+        else g[(size_t)(k - LST) * gs] = v;
+    }
+    __device__ __forceinline__ int get(int k) const { return k < LST ? l[k * kBlock] : g[(size_t)(k - LST) * gs]; }
+};
+
 // MODE 0: per-lane query kind (`any` may differ between lanes); 1: every lane
 // closest-hit; 2: every lane any-hit (phase-aligned shadow iterations).  Any-hit
 // queries need no visiting order, so mode 2 skips the sorting network.
 // Pushes write the slot above the top unconditionally and advance the stack
 // pointer by the hit predicate (no exec-mask branches); the highest slot written
 // is the same as with conditional pushes (<= 3 above the entry top).
-template <bool STATS, int MODE>
+// Slab test from precomputed plane distances (quantised nodes).
+__device__ __forceinline__ bool slab_t(float ax, float bx, float ay, float by, float az, float bz, float tmin,
+                                       float tmax, float& tn) {
+    float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+    float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * kGamma;
+    tfar = fminf(tfar, tmax * kGamma);
+    tn = tnear;
+    return tnear <= tfar;
+}
+__device__ __forceinline__ float ubyte(uint32_t w, int k) {
+    return (float)((w >> (8 * k)) & 0xFFu);   // v_cvt_f32_ubyte{k}
+}
+// Child k of a quantised node (prt_internal.h): plane distance (origin + q s - o) / d
+// evaluated as fma(q, s/d, (origin - o)/d); the >= 2 pad outward rounding of the grid
+// covers the estimate's error, so the test stays conservative.
+struct QAxis { float A, B; };
+__device__ __forceinline__ bool qchild(int k, uint32_t lxq, uint32_t hxq, uint32_t lyq, uint32_t hyq, uint32_t lzq,
+                                       uint32_t hzq, QAxis X, QAxis Y, QAxis Z, float tmin, float tmax, float& tn) {
+    return slab_t(__builtin_fmaf(ubyte(lxq, k), X.A, X.B), __builtin_fmaf(ubyte(hxq, k), X.A, X.B),
+                  __builtin_fmaf(ubyte(lyq, k), Y.A, Y.B), __builtin_fmaf(ubyte(hyq, k), Y.A, Y.B),
+                  __builtin_fmaf(ubyte(lzq, k), Z.A, Z.B), __builtin_fmaf(ubyte(hzq, k), Z.A, Z.B), tmin, tmax, tn);
+}
+
+template <bool STATS, int MODE, class S, bool QN = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                             V3 d, float tmin, float tmax, bool any_lane, int* lstack, int& hit_id,
+                                             V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
                                              float& hit_t, Counters& cn) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     V3 oi = o * inv;
     float best = tmax;
     int best_id = -1;
-    lstack[0] = kSentinel;
+    stk.put(0, kSentinel);
     int sp = 0;
     int cur = 0;
     int leaf = 0;
     do {
         while (cur >= 0 && cur != kSentinel) {
-            const float4* nd = nodes + (size_t)cur * 8;
-            float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5], rf = nd[6];
-            if (STATS) { cn.nodes++; cn.it_inner++; }
             float t0, t1, t2, t3;
-            bool h0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, oi, inv, tmin, best, t0);
-            bool h1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, oi, inv, tmin, best, t1);
-            bool h2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, oi, inv, tmin, best, t2);
-            bool h3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, oi, inv, tmin, best, t3);
-            int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z), r3 = __float_as_int(rf.w);
+            bool h0, h1, h2, h3;
+            int r0, r1, r2, r3;
+            if (QN) {
+                const float4* nd = nodes + (size_t)cur * 4;
+                float4 a = nd[0], b = nd[1], c = nd[2], rf = nd[3];
+                if (STATS) { cn.nodes++; cn.it_inner++; }
+                QAxis X = {a.w * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
+                QAxis Y = {b.x * inv.y, __builtin_fmaf(a.y, inv.y, -oi.y)};
+                QAxis Z = {b.y * inv.z, __builtin_fmaf(a.z, inv.z, -oi.z)};
+                uint32_t lxq = __float_as_uint(b.z), hxq = __float_as_uint(b.w);
+                uint32_t lyq = __float_as_uint(c.x), hyq = __float_as_uint(c.y);
+                uint32_t lzq = __float_as_uint(c.z), hzq = __float_as_uint(c.w);
+                r0 = __float_as_int(rf.x); r1 = __float_as_int(rf.y); r2 = __float_as_int(rf.z); r3 = __float_as_int(rf.w);
+                h0 = qchild(0, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t0) && r0 != kSentinel;
+                h1 = qchild(1, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t1) && r1 != kSentinel;
+                h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && r2 != kSentinel;
+                h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && r3 != kSentinel;
+            } else {
+                const float4* nd = nodes + (size_t)cur * 8;
+                float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5], rf = nd[6];
+                if (STATS) { cn.nodes++; cn.it_inner++; }
+                h0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, oi, inv, tmin, best, t0);
+                h1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, oi, inv, tmin, best, t1);
+                h2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, oi, inv, tmin, best, t2);
+                h3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, oi, inv, tmin, best, t3);
+                r0 = __float_as_int(rf.x); r1 = __float_as_int(rf.y); r2 = __float_as_int(rf.z); r3 = __float_as_int(rf.w);
+            }
             if (MODE == 2) {
-                lstack[(sp + 1) * kBlock] = r0; sp += h0 ? 1 : 0;
-                lstack[(sp + 1) * kBlock] = r1; sp += h1 ? 1 : 0;
-                lstack[(sp + 1) * kBlock] = r2; sp += h2 ? 1 : 0;
-                int top = lstack[sp * kBlock];
+                stk.put(sp + 1, r0); sp += h0 ? 1 : 0;
+                stk.put(sp + 1, r1); sp += h1 ? 1 : 0;
+                stk.put(sp + 1, r2); sp += h2 ? 1 : 0;
+                int top = stk.get(sp);
                 cur = h3 ? r3 : top;
                 sp -= h3 ? 0 : 1;
             } else {
@@ -521,16 +586,17 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 cswap(t1, r1, t3, r3);
                 cswap(t1, r1, t2, r2);
                 // hit children sorted near-to-far in r0..r(nh-1): visit r0, push the rest far-first
-                lstack[(sp + 1) * kBlock] = r3; sp += nh > 3 ? 1 : 0;
-                lstack[(sp + 1) * kBlock] = r2; sp += nh > 2 ? 1 : 0;
-                lstack[(sp + 1) * kBlock] = r1; sp += nh > 1 ? 1 : 0;
-                int top = lstack[sp * kBlock];
+                stk.put(sp + 1, r3); sp += nh > 3 ? 1 : 0;
+                stk.put(sp + 1, r2); sp += nh > 2 ? 1 : 0;
+                stk.put(sp + 1, r1); sp += nh > 1 ? 1 : 0;
+                int top = stk.get(sp);
                 cur = nh > 0 ? r0 : top;
                 sp -= nh > 0 ? 0 : 1;
             }
+            if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
-                cur = lstack[sp * kBlock];
+                cur = stk.get(sp);
                 --sp;
             }
             if (!__any(leaf >= 0)) break;
@@ -554,7 +620,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
             if (any && best_id >= 0) { leaf = 0; break; }
             leaf = cur;
             if (cur < 0) {
-                cur = lstack[sp * kBlock];
+                cur = stk.get(sp);
                 --sp;
             }
         }
@@ -653,12 +719,21 @@ void trace_kernel(TraceParams P) {
     // 4 BVH4 + parked state) | 8 for phase-aligned scheduling (see below)
     constexpr int TRAV = VAR & 7;
     constexpr bool PHASE = (VAR & 8) != 0;
+    constexpr bool SPILL = (VAR & 32) != 0;    // LDS stack of STACK entries + global spill area
+    constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
     // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
     // while the lane traverses, so traversal registers do not add to it.
     constexpr int kParkF4 = (TRAV == 4) ? 3 * kBlock : 0;
     int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
+    using StackT = typename std::conditional<SPILL, SpillStack<STACK>, LdsStack>::type;
+    StackT stk;
+    stk.l = lstack;
+    if constexpr (SPILL) {
+        stk.g = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
+        stk.gs = gridDim.x * kBlock;
+    }
     float4* park = smem + kStackWords * kBlock / 4 + threadIdx.x;
     const float4* g_nodes = P.nodes;
     const float4* g_tris = P.tris;
@@ -706,7 +781,7 @@ void trace_kernel(TraceParams P) {
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
     V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
     float tmax = kTMax;
-    Counters cn = {0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0};
     uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
     uint32_t chunk_s = 0;   // wave-uniform: sample index (within the launch) of the current chunk
     uint32_t chunk_xy0 = 0; // wave-uniform: origin of the current chunk's tile
@@ -820,16 +895,16 @@ void trace_kernel(TraceParams P) {
         } else if (TRAV == 2) {
             hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         } else if (TRAV == 3 && PHASE) {
-            if (do_shadow) hit = traverse_ww4<STATS, 2>(g_nodes, g_tris, o, d, kTMin, tmax, true, lstack, hid, ht, cn);
-            else hit = traverse_ww4<STATS, 1>(g_nodes, g_tris, o, d, kTMin, tmax, false, lstack, hid, ht, cn);
+            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn);
+            else hit = traverse_ww4<STATS, 1, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn);
         } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS, 0>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
         } else {
             park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
             park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
             park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
             asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS, 0>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
             asm volatile("" ::: "memory");
             float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
             beta = v3(k0.x, k0.y, k0.z);
@@ -1025,6 +1100,11 @@ void trace_kernel(TraceParams P) {
             for (int k = 0; k < 7; ++k) atomicAdd(P.stats + 4 + k, (unsigned long long)wv[k]);
         }
         {
+            uint32_t m = cn.max_sp;
+            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_down((int)m, off));
+            if (lane == 0) atomicMax(P.stats + 13, (unsigned long long)m);
+        }
+        {
             uint64_t a2 = l_inner, b2 = l_leaf;
             for (int off = 32; off > 0; off >>= 1) { a2 += __shfl_down(a2, off); b2 += __shfl_down(b2, off); }
             if (lane == 0) {
@@ -1071,18 +1151,36 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
     X(kVarWW4PhLds6, 11, true, 6)                        \
     X(kVarWW4PhLds, 11, true, 1)                         \
     X(kVarWW4Ph, 11, false, 1)                           \
-    X(kVarWW4Ph5, 11, false, 5)
+    X(kVarWW4Ph5, 11, false, 5)                          \
+    X(kVarWW4Sp, 35, false, 1)                           \
+    X(kVarWW4Sp4, 35, false, 4)                          \
+    X(kVarWW4Sp5, 35, false, 5)                          \
+    X(kVarWW4QSp, 99, false, 1)                          \
+    X(kVarWW4QSp5, 99, false, 5)                         \
+    X(kVarWW4QPhSp, 107, false, 1)                       \
+    X(kVarWW4QSp6, 99, false, 6)
+
+// spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
+template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
+static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStream_t stream) {
+    constexpr bool spill = (VAR & 32) != 0;
+    if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
+        trace_kernel<STACK, STATS, VAR, LDS, WPE><<<grid, kBlock, smem, stream>>>(P);
+        return hipGetLastError();
+    } else {
+        return hipErrorInvalidValue;
+    }
+}
 
 template <int STACK, bool STATS>
 static hipError_t launch_var(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream) {
     switch (var) {
 #define X(id, trav, lds, wpe) \
-        case id: trace_kernel<STACK, STATS, trav, lds, wpe><<<grid, kBlock, smem, stream>>>(P); break;
+        case id: return launch_one<STACK, STATS, trav, lds, wpe>(P, grid, smem, stream);
         PRT_VARIANTS(X)
 #undef X
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 template <int STACK>
@@ -1119,6 +1217,7 @@ size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream) {
     size_t smem = trace_smem_bytes(stack, var, P);
     switch (stack) {
+        case 4: return launch_stack<4>(P, var, grid, stats, smem, stream);
         case 10: return launch_stack<10>(P, var, grid, stats, smem, stream);
         case 16: return launch_stack<16>(P, var, grid, stats, smem, stream);
         case 32: return launch_stack<32>(P, var, grid, stats, smem, stream);
@@ -1138,12 +1237,19 @@ hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, b
     return hipGetLastError();
 }
 
+template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
+static void occ_one(int* n, size_t smem) {
+    constexpr bool spill = (VAR & 32) != 0;
+    if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(n, trace_kernel<STACK, STATS, VAR, LDS, WPE>, kBlock, smem);
+}
+
 template <int STACK, bool STATS>
 static int occ_var(int var, size_t smem) {
     int n = 0;
     switch (var) {
 #define X(id, trav, lds, wpe) \
-        case id: (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel<STACK, STATS, trav, lds, wpe>, kBlock, smem); break;
+        case id: occ_one<STACK, STATS, trav, lds, wpe>(&n, smem); break;
         PRT_VARIANTS(X)
 #undef X
         default: break;
@@ -1154,6 +1260,24 @@ static int occ_var(int var, size_t smem) {
 bool variant_uses_bvh4(int var) {
     switch (var) {
 #define X(id, trav, lds, wpe) case id: return (trav & 7) >= 3;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
+bool variant_quantized(int var) {
+    switch (var) {
+#define X(id, trav, lds, wpe) case id: return (trav & 64) != 0;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
+bool variant_spills(int var) {
+    switch (var) {
+#define X(id, trav, lds, wpe) case id: return (trav & 32) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;
@@ -1171,6 +1295,7 @@ bool variant_uses_lds(int var) {
 
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem) {
     switch (stack) {
+        case 4: return stats ? occ_var<4, true>(var, smem) : occ_var<4, false>(var, smem);
         case 10: return stats ? occ_var<10, true>(var, smem) : occ_var<10, false>(var, smem);
         case 16: return stats ? occ_var<16, true>(var, smem) : occ_var<16, false>(var, smem);
         case 32: return stats ? occ_var<32, true>(var, smem) : occ_var<32, false>(var, smem);

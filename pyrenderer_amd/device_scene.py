@@ -78,10 +78,11 @@ class DeviceScene:
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def kernel_info(self):
-        """Default trace-kernel variant: dict(variant, bvh_arity, lds_scene, stack)."""
+        """Default trace-kernel variant: dict(variant, bvh_arity, lds_scene, quantized, stack)."""
         out = np.zeros(4, np.int32)
         N.check(N.lib().prt_scene_kernel(self.h, N.ptr(out)))
-        return dict(variant=int(out[0]), bvh_arity=int(out[1]), lds_scene=bool(out[2]), stack=int(out[3]))
+        return dict(variant=int(out[0]), bvh_arity=int(out[1]), lds_scene=bool(out[2] & 1),
+                    quantized=bool(out[2] & 2), stack=int(out[3]))
 
     def kernel_timing(self):
         ms = ctypes.c_double(0.0)

@@ -193,7 +193,7 @@ def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
     cam = cornell[1].convert_to_taichi_camera().packed()
     ids = interleaved_tiles(64, 64, 32)
     o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
-    for v in range(1, 19):
+    for v in range(1, 26):
         g, _ = gpu_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
         assert np.array_equal(g, o), v
 
@@ -210,3 +210,17 @@ def test_general_camera_matches_oracle(gpu_scene, oracle_scene, cornell, mod):
     g = _gpu_frame(gpu_scene, cam, 40, 40, 2, 4, seed=3)
     o = oracle_scene.render(cam, 40, 40, 2, 4, seed=3)
     np.testing.assert_array_equal(g, o)
+
+
+def test_spill_stack_matches_oracle(cornell, oracle_scene, monkeypatch):
+    """Spill variants with a 4-entry LDS stack (PRT_SPILL_LDS=4): the Cornell box's
+    traversal stack reaches 8 entries, so the global spill area is exercised."""
+    from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
+    monkeypatch.setenv("PRT_SPILL_LDS", "4")
+    ds = DeviceScene(cornell[2], 0)
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    ids = interleaved_tiles(64, 64, 32)
+    o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
+    for v in (19, 20, 21):
+        g, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
+        assert np.array_equal(g, o), v
