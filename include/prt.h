@@ -126,6 +126,15 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
  * previous prt_kernel_timing() (synchronises on their events, then resets):
  * total ms and number of trace launches. */
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
+/* World.hit_all for a batch of rays (mathematics/intersection_taichi.py:238-291):
+ * rays = n x 8 f32 (o.xyz, t_min, d.xyz, t_max); hit_id = original triangle index,
+ * n_tri + k for sphere k, -1 for a miss; hit_t = distance (0 on a miss).  Closest hit
+ * = minimal (t, id) with the strict t_min < t < t_max test; PRT_HITS_ANY returns
+ * some hit in range instead (shadow queries).  PRT_HITS_QUANTIZED traverses the
+ * quantised BVH4 of large scenes instead of the f32 one (same results). */
+#define PRT_HITS_ANY 0x1u
+#define PRT_HITS_QUANTIZED 0x2u
+int prt_closest_hits(void* scene, const float* rays, int64_t n, uint32_t flags, int32_t* hit_id, float* hit_t);
 /* trace-kernel variant chosen for this scene when flags select none:
  * out4 = {variant, BVH arity (2 or 4), bit 0 scene LDS-resident | bit 1 quantised nodes,
  *         LDS traversal stack entries per lane} */

@@ -14,6 +14,8 @@ PRT_OK = 0
 PRT_FLAG_STATS = 0x1
 PRT_FLAG_TIME = 0x2
 PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
+PRT_HITS_ANY = 0x1
+PRT_HITS_QUANTIZED = 0x2
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
@@ -42,6 +44,7 @@ EXPORTS = {
     "prt_scene_create": (_i, [_i, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
     "prt_scene_info": (_i, [_vp, _vp]),
     "prt_scene_kernel": (_i, [_vp, _vp]),
+    "prt_closest_hits": (_i, [_vp, _vp, ctypes.c_int64, _u32, _vp, _vp]),
     "prt_scene_destroy": (None, [_vp]),
     "prt_render_tiles": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),

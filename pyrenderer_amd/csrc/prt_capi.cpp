@@ -102,6 +102,7 @@ struct Scene {
     int32_t depth4 = 0;
     int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
     int need4 = 0;                   // worst-case BVH4 traversal stack entries
+    int resume_min = 16;             // resume variants (env PRT_RESUME_MIN)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
     DevBuf spill;                    // spill variants: deep stack entries
     int64_t n_sph = 0;
@@ -177,7 +178,8 @@ bool lds_fits4(const Scene* s) { return lds_fits_var(s, true); }
 // LDS-resident scene when it fits; the >= 6 waves/SIMD build when six blocks' LDS
 // still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
 int default_variant(const Scene* s) {
-    if (!lds_fits4(s)) return prt::kVarWW4QSp5;  // global scene: 64-B quantised nodes, 16-entry LDS stack + spill
+    // global scene: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal tails
+    if (!lds_fits4(s)) return prt::kVarWW4QRSp5;
     if (!s->stack4) return prt::kVarWW;
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
@@ -239,6 +241,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
     {
         P.cam_fast = cam_fast ? 1 : 0;
+        P.resume_min = s->resume_min;
         P.rays = primary ? (const float4*)s->rays.p : nullptr;
         const float rd2 = -cam[18];
         for (int i = 0; i < 3; ++i) {
@@ -474,6 +477,7 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         s->cus = prop.multiProcessorCount;
         s->n_node_f4 = (int64_t)bvh.nodes.size() / 4;
         s->n_tri_f4 = (int64_t)bvh.tris.size() / 4;
+        if (const char* rm = std::getenv("PRT_RESUME_MIN")) s->resume_min = std::max(1, std::min(64, std::atoi(rm)));
         if (const char* sl = std::getenv("PRT_SPILL_LDS")) {
             int v = std::atoi(sl);
             s->spill_lds = v == 4 ? 4 : v == 32 ? 32 : 16;
@@ -499,6 +503,33 @@ int prt_scene_info(void* scene, int64_t* info8) {
     if (!s || !info8) return fail(PRT_ERR_ARG, "NULL argument");
     info8[0] = s->device; info8[1] = s->n_tri; info8[2] = s->n_nodes; info8[3] = s->depth;
     info8[4] = s->stack; info8[5] = (int64_t)s->device_bytes; info8[6] = s->blocks_per_cu; info8[7] = s->cus;
+    return PRT_OK;
+}
+
+int prt_closest_hits(void* scene, const float* rays, int64_t n, uint32_t flags, int32_t* hit_id, float* hit_t) {
+    auto* s = (Scene*)scene;
+    if (!s || (n > 0 && (!rays || !hit_id || !hit_t))) return fail(PRT_ERR_ARG, "NULL argument");
+    if (n < 0) return fail(PRT_ERR_ARG, "n < 0");
+    if (n == 0) return PRT_OK;
+    if (s->need4 > 64) return fail(PRT_ERR_ARG, "BVH4 too deep for the hit-query kernel");
+    DeviceGuard g(s->device);
+    const bool quant = (flags & PRT_HITS_QUANTIZED) != 0, any = (flags & PRT_HITS_ANY) != 0;
+    prt::TraceParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.nodes = (const float4*)(quant ? s->nodes4q.p : s->nodes4.p);
+    P.tris = (const float4*)s->tris.p;
+    P.n_tri = (int)s->n_tri;
+    P.n_sph = (int)s->n_sph;
+    P.sph = (const float4*)s->sph.p;
+    DevBuf d_rays, d_id, d_t;
+    HIP_TRY(d_rays.ensure(sizeof(float) * 8 * (size_t)n));
+    HIP_TRY(d_id.ensure(sizeof(int32_t) * (size_t)n));
+    HIP_TRY(d_t.ensure(sizeof(float) * (size_t)n));
+    HIP_TRY(hipMemcpyAsync(d_rays.p, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(prt::launch_hits(P, quant, any, 64, (const float4*)d_rays.p, n, (int*)d_id.p, (float*)d_t.p, s->stream));
+    HIP_TRY(hipMemcpyAsync(hit_id, d_id.p, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipMemcpyAsync(hit_t, d_t.p, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
     return PRT_OK;
 }
 

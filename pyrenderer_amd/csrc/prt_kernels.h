@@ -21,6 +21,7 @@ struct TraceParams {
     // the ray origin M (0,0,0,1) and the constant terms rd.z * M[i][2] of gen_ray,
     // evaluated on the host in the kernel's f32 order (camera_taichi.py:47-74)
     int cam_fast;
+    int resume_min;           // resume variants: leave the traversal loop below this many active lanes
     int* spill;               // spill variants: per-lane stack entries beyond the LDS part (stride = grid threads)
     const float4* rays;       // primary rays of this launch from camera_kernel, or null (generated in the refill)
     float cam_o[3], cam_k[3];
@@ -70,7 +71,10 @@ constexpr int kVarWW4QSp = 22;      // quantised 64-B BVH4 nodes, spill stack, g
 constexpr int kVarWW4QSp5 = 23;     // ... >= 5 waves per SIMD
 constexpr int kVarWW4QPhSp = 24;    // ... phase-aligned
 constexpr int kVarWW4QSp6 = 25;     // ... >= 6 waves per SIMD
-constexpr int kVarLast = 25;
+constexpr int kVarWW4PhRLds6 = 26;  // phase-aligned + suspended traversal tails (resume), LDS scene, >= 6 waves
+constexpr int kVarWW4RLds6 = 27;    // resume, mixed schedule, LDS scene, >= 6 waves
+constexpr int kVarWW4QRSp5 = 28;    // resume, quantised nodes, spill stack, >= 5 waves
+constexpr int kVarLast = 28;
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
 bool variant_quantized(int var);
@@ -79,6 +83,8 @@ bool variant_uses_bvh4(int var);
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);
 hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream);
+hipError_t launch_hits(const TraceParams& P, bool quantized, bool any, int stack, const float4* rays, int64_t n,
+                       int* hit_id, float* hit_t, hipStream_t stream);
 size_t lds_scene_bytes(const TraceParams& P);  // LDS-resident scene + shading data
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);

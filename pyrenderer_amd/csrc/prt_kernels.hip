@@ -207,17 +207,26 @@ __device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, f
 struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp; };
 
 // Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
+// t = (lo - o) / d is evaluated as fma(lo, 1/d, -o/d): pruning only, so the few-ulp
+// error of the estimate is covered by the box padding (~1e-6 of the scene scale,
+// >> |o/d| ulp) and the 1+2*gamma3 factor on t_far.  The near and far plane of each
+// axis are chosen by the sign of 1/d, NOT by min/max of the two distances: for a
+// direction component of exactly 0 (1/d = inf) a plane distance can be NaN, and
+// fminf/fmaxf would then turn the other plane's -inf into the FAR distance and cull
+// a box the ray lies inside (measured: 8 of 262144 pixels at config 2).  With the
+// selection, a NaN distance is dropped by the fmaxf/fminf that follow, which can
+// only enlarge the interval.  sx/sy/sz: 1/d.{x,y,z} < 0.
 __device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 oi, V3 inv,
                                      float tmin, float tmax, float& tn) {
-    // t = (lo - o) / d evaluated as fma(lo, 1/d, -o/d): pruning only, so the
-    // few-ulp error of the estimate is covered by the box padding (~1e-6 of the
-    // scene scale, >> |o/d| ulp) and the 1+2*gamma3 factor on t_far.
+    const bool sx = __float_as_int(inv.x) < 0, sy = __float_as_int(inv.y) < 0, sz = __float_as_int(inv.z) < 0;
     float ax = __builtin_fmaf(lx, inv.x, -oi.x), bx = __builtin_fmaf(hx, inv.x, -oi.x);
     float ay = __builtin_fmaf(ly, inv.y, -oi.y), by = __builtin_fmaf(hy, inv.y, -oi.y);
     float az = __builtin_fmaf(lz, inv.z, -oi.z), bz = __builtin_fmaf(hz, inv.z, -oi.z);
-    float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
-    float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * kGamma;
-    tfar = fminf(tfar, tmax * kGamma);
+    float nx = sx ? bx : ax, fx = sx ? ax : bx;
+    float ny = sy ? by : ay, fy = sy ? ay : by;
+    float nz = sz ? bz : az, fz = sz ? az : bz;
+    float tnear = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
+    float tfar = fminf(fminf(fx, fy), fminf(fz, tmax)) * kGamma;   // min(a g, b g) = min(a, b) g (g > 0)
     tn = tnear;
     return tnear <= tfar;
 }
@@ -501,12 +510,11 @@ struct SpillStack {
 // Pushes write the slot above the top unconditionally and advance the stack
 // pointer by the hit predicate (no exec-mask branches); the highest slot written
 // is the same as with conditional pushes (<= 3 above the entry top).
-// Slab test from precomputed plane distances (quantised nodes).
-__device__ __forceinline__ bool slab_t(float ax, float bx, float ay, float by, float az, float bz, float tmin,
+// Slab test from plane distances already ordered near/far (quantised nodes).
+__device__ __forceinline__ bool slab_t(float nx, float fx, float ny, float fy, float nz, float fz, float tmin,
                                        float tmax, float& tn) {
-    float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
-    float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz)) * kGamma;
-    tfar = fminf(tfar, tmax * kGamma);
+    float tnear = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
+    float tfar = fminf(fminf(fx, fy), fminf(fz, tmax)) * kGamma;
     tn = tnear;
     return tnear <= tfar;
 }
@@ -515,7 +523,8 @@ __device__ __forceinline__ float ubyte(uint32_t w, int k) {
 }
 // Child k of a quantised node (prt_internal.h): plane distance (origin + q s - o) / d
 // evaluated as fma(q, s/d, (origin - o)/d); the >= 2 pad outward rounding of the grid
-// covers the estimate's error, so the test stays conservative.
+// covers the estimate's error, so the test stays conservative.  The q words arrive
+// already swapped into near/far order by the sign of 1/d (see slab()).
 struct QAxis { float A, B; };
 __device__ __forceinline__ bool qchild(int k, uint32_t lxq, uint32_t hxq, uint32_t lyq, uint32_t hyq, uint32_t lzq,
                                        uint32_t hzq, QAxis X, QAxis Y, QAxis Z, float tmin, float tmax, float& tn) {
@@ -524,19 +533,50 @@ __device__ __forceinline__ bool qchild(int k, uint32_t lxq, uint32_t hxq, uint32
                   __builtin_fmaf(ubyte(lzq, k), Z.A, Z.B), __builtin_fmaf(ubyte(hzq, k), Z.A, Z.B), tmin, tmax, tn);
 }
 
-template <bool STATS, int MODE, class S, bool QN = false>
+// Traversal state of a query that may be suspended between loop iterations (RES).
+struct TState { int cur, leaf, sp, best_id; float best; };
+template <class S>
+__device__ __forceinline__ void tstate_init(TState& ts, S stk, float tmax) {
+    stk.put(0, kSentinel);
+    ts.cur = 0; ts.leaf = 0; ts.sp = 0; ts.best_id = -1; ts.best = tmax;
+}
+
+// RES: the wave leaves the traversal loop once fewer than `min_lanes` lanes are still
+// traversing; the unfinished lanes keep their state (registers + LDS stack) and resume
+// in the next iteration, so the long tail of a few slow lanes no longer idles the
+// others.  Returns whether the query finished (hit_id / hit_t valid).
+// Slab test with the near/far planes already selected by the sign of 1/d (BVH4
+// nodes: the selection is an address offset, no per-plane selects); same values as
+// slab().
+__device__ __forceinline__ bool slab_nf(float nx, float fx, float ny, float fy, float nz, float fz, V3 oi, V3 inv,
+                                        float tmin, float tmax, float& tn) {
+    float ax = __builtin_fmaf(nx, inv.x, -oi.x), bx = __builtin_fmaf(fx, inv.x, -oi.x);
+    float ay = __builtin_fmaf(ny, inv.y, -oi.y), by = __builtin_fmaf(fy, inv.y, -oi.y);
+    float az = __builtin_fmaf(nz, inv.z, -oi.z), bz = __builtin_fmaf(fz, inv.z, -oi.z);
+    float tnear = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin));
+    float tfar = fminf(fminf(bx, by), fminf(bz, tmax)) * kGamma;
+    tn = tnear;
+    return tnear <= tfar;
+}
+
+template <bool STATS, int MODE, class S, bool QN = false, bool RES = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
-                                             float& hit_t, Counters& cn) {
+                                             float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     V3 oi = o * inv;
-    float best = tmax;
-    int best_id = -1;
-    stk.put(0, kSentinel);
-    int sp = 0;
-    int cur = 0;
-    int leaf = 0;
+    // near plane index per axis (0 = lo, 1 = hi) from the sign of 1/d
+    const int sx = __float_as_int(inv.x) < 0 ? 1 : 0, sy = __float_as_int(inv.y) < 0 ? 1 : 0,
+              sz = __float_as_int(inv.z) < 0 ? 1 : 0;
+    TState ts;
+    if (RES) ts = *tsp;
+    else tstate_init(ts, stk, tmax);
+    float best = ts.best;
+    int best_id = ts.best_id;
+    int sp = ts.sp;
+    int cur = ts.cur;
+    int leaf = ts.leaf;
     do {
         while (cur >= 0 && cur != kSentinel) {
             float t0, t1, t2, t3;
@@ -549,22 +589,24 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 QAxis X = {a.w * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
                 QAxis Y = {b.x * inv.y, __builtin_fmaf(a.y, inv.y, -oi.y)};
                 QAxis Z = {b.y * inv.z, __builtin_fmaf(a.z, inv.z, -oi.z)};
-                uint32_t lxq = __float_as_uint(b.z), hxq = __float_as_uint(b.w);
-                uint32_t lyq = __float_as_uint(c.x), hyq = __float_as_uint(c.y);
-                uint32_t lzq = __float_as_uint(c.z), hzq = __float_as_uint(c.w);
+                uint32_t lxq = __float_as_uint(sx ? b.w : b.z), hxq = __float_as_uint(sx ? b.z : b.w);
+                uint32_t lyq = __float_as_uint(sy ? c.y : c.x), hyq = __float_as_uint(sy ? c.x : c.y);
+                uint32_t lzq = __float_as_uint(sz ? c.w : c.z), hzq = __float_as_uint(sz ? c.z : c.w);
                 r0 = __float_as_int(rf.x); r1 = __float_as_int(rf.y); r2 = __float_as_int(rf.z); r3 = __float_as_int(rf.w);
                 h0 = qchild(0, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t0) && r0 != kSentinel;
                 h1 = qchild(1, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t1) && r1 != kSentinel;
                 h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && r2 != kSentinel;
                 h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && r3 != kSentinel;
             } else {
+                // near/far planes picked by address (the node stores lo and hi per axis)
                 const float4* nd = nodes + (size_t)cur * 8;
-                float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5], rf = nd[6];
+                float4 nx = nd[sx], fx = nd[1 - sx], ny = nd[2 + sy], fy = nd[3 - sy], nz = nd[4 + sz], fz = nd[5 - sz];
+                float4 rf = nd[6];
                 if (STATS) { cn.nodes++; cn.it_inner++; }
-                h0 = slab(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, oi, inv, tmin, best, t0);
-                h1 = slab(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, oi, inv, tmin, best, t1);
-                h2 = slab(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, oi, inv, tmin, best, t2);
-                h3 = slab(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, oi, inv, tmin, best, t3);
+                h0 = slab_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, oi, inv, tmin, best, t0);
+                h1 = slab_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, oi, inv, tmin, best, t1);
+                h2 = slab_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, oi, inv, tmin, best, t2);
+                h3 = slab_nf(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, oi, inv, tmin, best, t3);
                 r0 = __float_as_int(rf.x); r1 = __float_as_int(rf.y); r2 = __float_as_int(rf.z); r3 = __float_as_int(rf.w);
             }
             if (MODE == 2) {
@@ -580,15 +622,13 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 t2 = h2 ? t2 : INFINITY;
                 t3 = h3 ? t3 : INFINITY;
                 int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
+                // nearest hit child first (3 comparators); the other hits pushed in slot order
                 cswap(t0, r0, t1, r1);
                 cswap(t2, r2, t3, r3);
                 cswap(t0, r0, t2, r2);
-                cswap(t1, r1, t3, r3);
-                cswap(t1, r1, t2, r2);
-                // hit children sorted near-to-far in r0..r(nh-1): visit r0, push the rest far-first
-                stk.put(sp + 1, r3); sp += nh > 3 ? 1 : 0;
-                stk.put(sp + 1, r2); sp += nh > 2 ? 1 : 0;
-                stk.put(sp + 1, r1); sp += nh > 1 ? 1 : 0;
+                stk.put(sp + 1, r3); sp += t3 != INFINITY ? 1 : 0;
+                stk.put(sp + 1, r2); sp += t2 != INFINITY ? 1 : 0;
+                stk.put(sp + 1, r1); sp += t1 != INFINITY ? 1 : 0;
                 int top = stk.get(sp);
                 cur = nh > 0 ? r0 : top;
                 sp -= nh > 0 ? 0 : 1;
@@ -624,9 +664,14 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 --sp;
             }
         }
+        if (RES && (cur != kSentinel || leaf < 0) && __popcll(__ballot(true)) < min_lanes) break;
     } while (cur != kSentinel || leaf < 0);
     hit_id = best_id;
     hit_t = best;
+    if (RES) {
+        tsp->cur = cur; tsp->leaf = leaf; tsp->sp = sp; tsp->best_id = best_id; tsp->best = best;
+        return !(cur != kSentinel || leaf < 0);
+    }
     return best_id >= 0;
 }
 
@@ -721,6 +766,7 @@ void trace_kernel(TraceParams P) {
     constexpr bool PHASE = (VAR & 8) != 0;
     constexpr bool SPILL = (VAR & 32) != 0;    // LDS stack of STACK entries + global spill area
     constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
+    constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
     // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
@@ -775,6 +821,8 @@ void trace_kernel(TraceParams P) {
     bool exhausted = false;
 
     // lane state
+    TState tst = {0, 0, 0, -1, 0.0f};
+    bool pending = false;   // RESUME: a suspended query (state in tst + the LDS stack)
     int item = -1;
     int bounce = 0, qtype = Q_EXT;
     uint32_t st = 0;
@@ -875,7 +923,9 @@ void trace_kernel(TraceParams P) {
         float ht = 0.0f;
         bool hit;
         if (STATS) {
-            if (qtype == Q_EXT) cn.ext++; else cn.shadow++;
+            if (!pending) {
+                if (qtype == Q_EXT) cn.ext++; else cn.shadow++;
+            }
             // wave-level clocks: the first active lane books the interval
             const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
             const uint64_t active = __ballot(true);
@@ -894,17 +944,32 @@ void trace_kernel(TraceParams P) {
             hit = traverse_u<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         } else if (TRAV == 2) {
             hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
+        } else if (TRAV == 3 && RESUME) {
+            if (!pending) tstate_init(tst, stk, tmax);
+            bool done;
+            if (PHASE && do_shadow)
+                done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn,
+                                                                  &tst, P.resume_min);
+            else if (PHASE)
+                done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht,
+                                                                  cn, &tst, P.resume_min);
+            else
+                done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk,
+                                                                  hid, ht, cn, &tst, P.resume_min);
+            pending = !done;
+            if (pending) continue;   // resume next iteration; no shading yet
+            hit = hid >= 0;
         } else if (TRAV == 3 && PHASE) {
-            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn);
-            else hit = traverse_ww4<STATS, 1, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn);
+            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn);
+            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn);
         } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
         } else {
             park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
             park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
             park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
             asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS, 0, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
             asm volatile("" ::: "memory");
             float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
             beta = v3(k0.x, k0.y, k0.z);
@@ -1115,6 +1180,39 @@ void trace_kernel(TraceParams P) {
     }
 }
 
+// World.hit_all for a batch of rays (intersection_taichi.py:238-291): closest (or any)
+// hit over the BVH4 (float or quantised nodes) then the spheres, one ray per lane.
+// rays: n x (o.xyz, tmin), (d.xyz, tmax).  Used by the hit-level parity tests.
+template <bool QN, bool ANY>
+__global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float4* __restrict__ rays, int64_t n,
+                                                      int* __restrict__ hit_id, float* __restrict__ hit_t) {
+    extern __shared__ float4 smem[];
+    int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    LdsStack stk{reinterpret_cast<int*>(smem) + threadIdx.x};
+    if (i >= n) return;
+    float4 a = rays[2 * i], b = rays[2 * i + 1];
+    V3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+    Counters cn = {0, 0, 0, 0, 0, 0, 0};
+    int hid = -1;
+    float ht = 0.0f;
+    bool hit = traverse_ww4<false, ANY ? 2 : 1, LdsStack, QN>(P.nodes, P.tris, o, d, a.w, b.w, ANY, stk, hid, ht, cn);
+    if (P.n_sph > 0 && !(ANY && hit)) {
+        float best = hit ? ht : b.w;
+        for (int k = 0; k < P.n_sph; ++k) {
+            float root;
+            if (sphere_hit(P.sph[k], o, d, a.w, best, root)) {
+                best = root;
+                hid = P.n_tri + k;
+                hit = true;
+                if (ANY) break;
+            }
+        }
+        ht = best;
+    }
+    hit_id[i] = hit ? hid : -1;
+    hit_t[i] = hit ? ht : 0.0f;
+}
+
 // Sequential per-pixel sum over this chunk's samples, in sample order, onto
 // the running sums (bit-identical to acc = acc + L[s] for s = 0..spp-1).
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict__ buf, float* __restrict__ acc,
@@ -1158,7 +1256,10 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
     X(kVarWW4QSp, 99, false, 1)                          \
     X(kVarWW4QSp5, 99, false, 5)                         \
     X(kVarWW4QPhSp, 107, false, 1)                       \
-    X(kVarWW4QSp6, 99, false, 6)
+    X(kVarWW4QSp6, 99, false, 6)                         \
+    X(kVarWW4PhRLds6, 139, true, 6)                      \
+    X(kVarWW4RLds6, 131, true, 6)                        \
+    X(kVarWW4QRSp5, 227, false, 5)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
@@ -1223,6 +1324,21 @@ hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool
         case 32: return launch_stack<32>(P, var, grid, stats, smem, stream);
         default: return launch_stack<64>(P, var, grid, stats, smem, stream);
     }
+}
+
+hipError_t launch_hits(const TraceParams& P, bool quantized, bool any, int stack, const float4* rays, int64_t n,
+                       int* hit_id, float* hit_t, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+    size_t smem = (size_t)stack * kBlock * sizeof(int);
+    if (quantized) {
+        if (any) hits_kernel<true, true><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
+        else hits_kernel<true, false><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
+    } else {
+        if (any) hits_kernel<false, true><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
+        else hits_kernel<false, false><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream) {

@@ -77,6 +77,22 @@ class DeviceScene:
                                                 spp, depth, int(seed), flags, ctypes.c_void_p(d_out_ptr),
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def closest_hits(self, o, d, tmin, tmax, any_hit=False, quantized=False):
+        """World.hit_all on the GPU for arrays of rays: (hit_id, t); id -1 = miss."""
+        o = np.asarray(o, np.float32).reshape(-1, 3)
+        d = np.asarray(d, np.float32).reshape(-1, 3)
+        n = o.shape[0]
+        rays = np.zeros((n, 8), np.float32)
+        rays[:, 0:3] = o
+        rays[:, 3] = np.broadcast_to(np.asarray(tmin, np.float32), (n,))
+        rays[:, 4:7] = d
+        rays[:, 7] = np.broadcast_to(np.asarray(tmax, np.float32), (n,))
+        hid = np.zeros(n, np.int32)
+        ht = np.zeros(n, np.float32)
+        flags = (N.PRT_HITS_ANY if any_hit else 0) | (N.PRT_HITS_QUANTIZED if quantized else 0)
+        N.check(N.lib().prt_closest_hits(self.h, N.ptr(rays), n, flags, N.ptr(hid), N.ptr(ht)))
+        return hid, ht
+
     def kernel_info(self):
         """Default trace-kernel variant: dict(variant, bvh_arity, lds_scene, quantized, stack)."""
         out = np.zeros(4, np.int32)

@@ -135,24 +135,20 @@ def test_triangle_soup_matches_oracle(cornell):
     assert same >= 0.999, same
 
 
-def test_full_size_config2_properties(gpu_scene, oracle_scene, cornell):
-    """BASELINE config 2 at full size (512^2 x 64 spp, depth 8): finite, deterministic,
-    and bit-identical to the oracle on a random sample of 8x8 tiles."""
-    from pyrenderer_amd.device_scene import interleaved_tiles, unpack_tiles
+def test_full_size_config2_matches_oracle(gpu_scene, oracle_scene, cornell):
+    """BASELINE config 2 at full size (512^2 x 64 spp, depth 8), the WHOLE frame
+    against the oracle (brute-force closest hits, all host threads).  At this size
+    rare events (e.g. a direction component of exactly 0, ~2^-24 per draw) occur a
+    few times, so a sampled check is not enough."""
+    import os
     cam = cornell[1].convert_to_taichi_camera().packed()
     W = H = 512
     full = _gpu_frame(gpu_scene, cam, W, H, 64, 8, seed=0)
     assert np.isfinite(full).all() and full.mean() > 0
-    rng = np.random.default_rng(0)
-    ids = np.sort(rng.choice((W // 8) * (H // 8), 12, replace=False)).astype(np.int32)
-    o = oracle_scene.render_tiles(cam, W, H, 8, 8, ids, 64, 8, seed=0)
-    sub = np.zeros((W, H, 3), np.float32)
-    unpack_tiles(o, W, H, 8, 8, ids, sub)
-    mask = np.zeros((W, H), bool)
-    tx = W // 8
-    for t in ids:
-        mask[(t % tx) * 8:(t % tx) * 8 + 8, (t // tx) * 8:(t // tx) * 8 + 8] = True
-    assert np.array_equal(full[mask], sub[mask])
+    nthreads = min(16, len(os.sched_getaffinity(0)))
+    o = oracle_scene.render(cam, W, H, 64, 8, seed=0, nthreads=nthreads)
+    diff = np.any(full != o, axis=-1)
+    assert not diff.any(), (int(diff.sum()), np.argwhere(diff)[:5])
 
 
 def _specular_scene(rough=0.0):
@@ -193,7 +189,7 @@ def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
     cam = cornell[1].convert_to_taichi_camera().packed()
     ids = interleaved_tiles(64, 64, 32)
     o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
-    for v in range(1, 26):
+    for v in range(1, 29):
         g, _ = gpu_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
         assert np.array_equal(g, o), v
 
