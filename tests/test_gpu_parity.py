@@ -189,7 +189,7 @@ def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
     cam = cornell[1].convert_to_taichi_camera().packed()
     ids = interleaved_tiles(64, 64, 32)
     o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
-    for v in range(1, 29):
+    for v in range(1, 31):
         g, _ = gpu_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
         assert np.array_equal(g, o), v
 
