@@ -36,6 +36,7 @@ extern "C" {
 #define PRT_ERR_OOM (-3)     /* host or device allocation failed */
 #define PRT_ERR_RCCL (-4)    /* RCCL communicator / collective failure */
 #define PRT_ERR_UNSUP (-5)   /* feature not supported by this build */
+#define PRT_ERR_INTERNAL (-6) /* device-side check failed (traversal watchdog); results invalid */
 
 /* render flags */
 #define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
@@ -124,7 +125,9 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
                             uint32_t flags, float* d_out_sum, void* stream);
 /* trace-kernel time of every render call made with PRT_FLAG_TIME since the
  * previous prt_kernel_timing() (synchronises on their events, then resets):
- * total ms and number of trace launches. */
+ * total ms and number of trace launches.  Also reports PRT_ERR_INTERNAL if the
+ * traversal watchdog tripped in the last render (device-output renders are not
+ * checked otherwise). */
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
 /* World.hit_all for a batch of rays (mathematics/intersection_taichi.py:238-291):
  * rays = n x 8 f32 (o.xyz, t_min, d.xyz, t_max); hit_id = original triangle index,

@@ -328,10 +328,14 @@ void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
         for (int k = 0; k < 4; ++k) {
             bool ok = k < (int)ch.size();
             for (int a = 0; a < 3; ++a) {
+                // empty slot: inverted box (lo = +inf, hi = -inf) is missed by every ray
+                // whose direction has one finite 1/d, whatever t_max (even NaN / inf)
                 f[(2 * a) * 4 + k] = ok ? ch[k].lo[a] : INFINITY;
-                f[(2 * a + 1) * 4 + k] = ok ? ch[k].hi[a] : INFINITY;
+                f[(2 * a + 1) * 4 + k] = ok ? ch[k].hi[a] : -INFINITY;
             }
-            int32_t ref = 0;
+            // empty slot ref = the traversal sentinel: if a NaN ray ever "hits" it, the lane's
+            // traversal ends instead of restarting at the root (a NaN ray hits nothing anyway)
+            int32_t ref = 0x7FFFFFFF;
             if (ok) {
                 if (ch[k].ref >= 0) {
                     ref = (int32_t)out->n_nodes++;

@@ -157,6 +157,15 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
     return PRT_OK;
 }
 
+// work.p: [0] chunk counter; [kFaultOffset] traversal watchdog flag
+constexpr size_t kFaultOffset = 32;
+
+int read_fault(Scene* s) {
+    int f = 0;
+    if (hipMemcpy(&f, (char*)s->work.p + kFaultOffset, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return f;
+}
+
 // LDS-resident scene: BVH + triangles small enough to sit beside the stack
 constexpr int64_t kLdsSceneBytes = 24 * 1024;
 void scene_sizes(const Scene* s, bool bvh4, prt::TraceParams& P) {
@@ -226,6 +235,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     const bool stats = (flags & PRT_FLAG_STATS) != 0;
     const bool timed = (flags & PRT_FLAG_TIME) != 0;
     if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), stream));
+    HIP_TRY(hipMemsetAsync((char*)s->work.p + kFaultOffset, 0, sizeof(int), stream));
 
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
@@ -259,6 +269,7 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.depth = depth;
     P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
     P.work = (uint32_t*)s->work.p;
+    P.fault = (int*)((char*)s->work.p + kFaultOffset);
     P.out = (float*)s->buf.p;
     P.stats = (unsigned long long*)s->stats.p;
     scene_sizes(s, false, P);
@@ -525,11 +536,14 @@ int prt_closest_hits(void* scene, const float* rays, int64_t n, uint32_t flags, 
     HIP_TRY(d_rays.ensure(sizeof(float) * 8 * (size_t)n));
     HIP_TRY(d_id.ensure(sizeof(int32_t) * (size_t)n));
     HIP_TRY(d_t.ensure(sizeof(float) * (size_t)n));
+    P.fault = (int*)((char*)s->work.p + kFaultOffset);
+    HIP_TRY(hipMemsetAsync(P.fault, 0, sizeof(int), s->stream));
     HIP_TRY(hipMemcpyAsync(d_rays.p, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice, s->stream));
     HIP_TRY(prt::launch_hits(P, quant, any, 64, (const float4*)d_rays.p, n, (int*)d_id.p, (float*)d_t.p, s->stream));
     HIP_TRY(hipMemcpyAsync(hit_id, d_id.p, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipMemcpyAsync(hit_t, d_t.p, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (read_fault(s) != 0) return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     return PRT_OK;
 }
 
@@ -562,6 +576,7 @@ int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th
     if (n_slots)
         HIP_TRY(hipMemcpyAsync(out_sum, s->acc.p, sizeof(float) * 3 * (size_t)n_slots, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (read_fault(s) != 0) return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     if (stats) {
         if (flags & PRT_FLAG_STATS) {
             unsigned long long h[4];
@@ -599,6 +614,10 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
     }
     *ms_total = tot;
     *launches = s->ev_used / 2;
+    if (read_fault(s) != 0) {
+        s->ev_used = 0;
+        return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
+    }
     s->ev_used = 0;
     return PRT_OK;
 }

@@ -38,7 +38,8 @@ struct BvhHost {
 // BVH4 collapsed from the BVH2 (same triangle order and leaf encoding).
 // One node = 8 x float4 = 128 B, children in SoA so one node fetch tests
 // four boxes: f[0..5] = lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4];
-// f[6] = child refs (int bits); f[7] = unused.  Empty slots have lo = hi = +inf.
+// f[6] = child refs (int bits); f[7] = unused.  Empty slots: lo = +inf, hi = -inf,
+// ref = 0x7FFFFFFF (the traversal sentinel).
 constexpr int kNode4F4 = 8;
 struct Bvh4Host {
     std::vector<float> nodes;      // n_nodes * 32

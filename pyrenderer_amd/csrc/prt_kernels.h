@@ -21,6 +21,7 @@ struct TraceParams {
     // the ray origin M (0,0,0,1) and the constant terms rd.z * M[i][2] of gen_ray,
     // evaluated on the host in the kernel's f32 order (camera_taichi.py:47-74)
     int cam_fast;
+    int* fault;               // watchdog flag (non-zero: a traversal exceeded kGuardTrips)
     int resume_min;           // resume variants: leave the traversal loop below this many active lanes
     int* spill;               // spill variants: per-lane stack entries beyond the LDS part (stride = grid threads)
     const float4* rays;       // primary rays of this launch from camera_kernel, or null (generated in the refill)

@@ -398,6 +398,7 @@ __device__ __forceinline__ bool traverse_u(const float4* __restrict__ nodes, con
 // of different lanes do not serialise against each other.  Stack bottom
 // holds kSentinel; leaves are negative references, inner nodes >= 0.
 constexpr int kSentinel = 0x7FFFFFFF;
+constexpr uint32_t kGuardTrips = 1u << 20;   // leaf batches per query before the watchdog trips
 
 template <bool STATS>
 __device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
@@ -562,7 +563,8 @@ __device__ __forceinline__ bool slab_nf(float nx, float fx, float ny, float fy, 
 template <bool STATS, int MODE, class S, bool QN = false, bool RES = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
-                                             float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0) {
+                                             float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0,
+                                             int* fault = nullptr) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     V3 oi = o * inv;
@@ -574,6 +576,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     else tstate_init(ts, stk, tmax);
     float best = ts.best;
     int best_id = ts.best_id;
+    uint32_t guard = 0;
     int sp = ts.sp;
     int cur = ts.cur;
     int leaf = ts.leaf;
@@ -665,6 +668,13 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
             }
         }
         if (RES && (cur != kSentinel || leaf < 0) && __popcll(__ballot(true)) < min_lanes) break;
+        // watchdog: a traversal revisiting nodes forever (corrupt tree) ends the query and
+        // raises the fault flag that the host turns into an error, instead of hanging the GPU
+        if (++guard > kGuardTrips) {
+            if (fault) atomicOr(fault, 1);
+            cur = kSentinel;
+            leaf = 0;
+        }
     } while (cur != kSentinel || leaf < 0);
     hit_id = best_id;
     hit_t = best;
@@ -949,27 +959,27 @@ void trace_kernel(TraceParams P) {
             bool done;
             if (PHASE && do_shadow)
                 done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn,
-                                                                  &tst, P.resume_min);
+                                                                  &tst, P.resume_min, P.fault);
             else if (PHASE)
                 done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht,
-                                                                  cn, &tst, P.resume_min);
+                                                                  cn, &tst, P.resume_min, P.fault);
             else
                 done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk,
-                                                                  hid, ht, cn, &tst, P.resume_min);
+                                                                  hid, ht, cn, &tst, P.resume_min, P.fault);
             pending = !done;
             if (pending) continue;   // resume next iteration; no shading yet
             hit = hid >= 0;
         } else if (TRAV == 3 && PHASE) {
-            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn);
-            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn);
+            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn, nullptr, 0, P.fault);
+            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn, nullptr, 0, P.fault);
         } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault);
         } else {
             park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
             park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
             park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
             asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault);
             asm volatile("" ::: "memory");
             float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
             beta = v3(k0.x, k0.y, k0.z);
@@ -1195,7 +1205,8 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float
     Counters cn = {0, 0, 0, 0, 0, 0, 0};
     int hid = -1;
     float ht = 0.0f;
-    bool hit = traverse_ww4<false, ANY ? 2 : 1, LdsStack, QN>(P.nodes, P.tris, o, d, a.w, b.w, ANY, stk, hid, ht, cn);
+    bool hit = traverse_ww4<false, ANY ? 2 : 1, LdsStack, QN>(P.nodes, P.tris, o, d, a.w, b.w, ANY, stk, hid, ht, cn,
+                                                              nullptr, 0, P.fault);
     if (P.n_sph > 0 && !(ANY && hit)) {
         float best = hit ? ht : b.w;
         for (int k = 0; k < P.n_sph; ++k) {

@@ -220,3 +220,16 @@ def test_spill_stack_matches_oracle(cornell, oracle_scene, monkeypatch):
     for v in (19, 20, 21):
         g, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
         assert np.array_equal(g, o), v
+
+
+def test_large_frame_matches_oracle(gpu_scene, oracle_scene, cornell):
+    """1024^2 x 32 spp (33.5 M samples): contains shadow rays with t_max = NaN
+    (p2.x == p.x), which once made BVH4 empty slots (then ref = root) 'hit' and the
+    traversal loop forever.  Whole frame against the oracle."""
+    import os
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    W = H = 1024
+    g = _gpu_frame(gpu_scene, cam, W, H, 32, 8, seed=0)
+    o = oracle_scene.render(cam, W, H, 32, 8, seed=0, nthreads=min(16, len(os.sched_getaffinity(0))))
+    diff = np.any(g != o, axis=-1)
+    assert not diff.any(), (int(diff.sum()), np.argwhere(diff)[:5])
