@@ -2,9 +2,12 @@
 depth 8 (BASELINE.json configs[1]), on N GPUs of one node.
 
 One step = one full frame: every rank renders its interleaved 64x64 tiles
-(tile id % N == rank) through libprt's HIP path into a device buffer, then the
-per-tile radiance sums are gathered to rank 0 over RCCL (torch.distributed
-'nccl' backend).  Total work is fixed as N grows ("scaling": "strong").
+(device_scene.tile_owner, 'latin' scheme) through libprt's HIP path into a device
+buffer, then the per-tile radiance sums are gathered to rank 0 over RCCL
+(torch.distributed 'nccl' backend).  Total work is fixed as N grows ("scaling":
+"strong").  Consecutive frames alternate between --streams HIP streams, each with
+its own buffers, so the drain of frame k (the last paths of a persistent launch,
+~0.3 ms at any frame size) and its gather overlap the start of frame k+1.
 
     python bench.py --gpus 1 --steps 10 --warmup 3
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
@@ -72,6 +75,9 @@ def parse():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--streams", type=int, default=2, help="frames in flight (1 = strictly serial frames)")
+    ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
+    ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -158,14 +164,20 @@ def main():
     t_build = time.perf_counter() - t_build
     W = H = args.res
     T = args.tile
-    shard = TileShard(W, H, T, rank, world, dev)
-    my_tiles = shard.tiles
-    stream = torch.cuda.current_stream(dev)
+    n_streams = max(1, args.streams)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
+    shards = [TileShard(W, H, T, rank, world, dev, args.scheme) for _ in range(n_streams)]
+    my_tiles = shards[0].tiles
+    n_step = [0]
 
     def step(flags=0):
+        k = n_step[0] % n_streams
+        n_step[0] += 1
+        shard, stream = shards[k], streams[k]
         ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, shard.buf.data_ptr(),
-                               stream.cuda_stream, seed=args.seed, flags=flags)
-        shard.gather()    # RCCL gather of per-tile radiance sums to rank 0
+                               stream.cuda_stream, seed=args.seed, flags=flags | (args.variant << 8))
+        with torch.cuda.stream(stream):
+            shard.gather()    # RCCL gather of per-tile radiance sums to rank 0 (ordered after this frame)
 
     # counted traversal work of one frame (deterministic: same RNG as the timed steps)
     step(N.PRT_FLAG_STATS)
@@ -205,6 +217,8 @@ def main():
         per_rank = 1.0 / world
         n_px_rank = len(my_tiles) * T * T
         kinfo = ds.kernel_info()
+        if args.variant:
+            kinfo = dict(kinfo, variant=args.variant)
         arity = kinfo["bvh_arity"]
         b_node = (B_NODE4Q if kinfo["quantized"] else B_NODE4) if arity == 4 else B_NODE2
         bytes_launch = ((b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank
@@ -231,10 +245,13 @@ def main():
             "config": {"workload": f"{SCENE_NAMES[args.scene]} {W}x{H}, {args.spp} spp, depth {args.depth}",
                        "baseline_config": args.config, "triangles": int(flat.n_tri), "spheres": int(flat.sph.shape[0]),
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
+                       "tile_scheme": args.scheme, "frames_in_flight": n_streams,
                        "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "trace_kernel", "kernel_avg_ms": round(kern_avg_ms, 4),
+                         "kernel_avg_note": "HIP-event duration of each trace launch on its stream; with frames "
+                                            "in flight a launch's span includes time shared with the next frame",
                          "bytes_per_launch": int(bytes_launch), "launches_per_step": round(launches_per_step, 3),
                          "variant": kinfo,
                          "note": "achieved = logical scene + sample-buffer bytes (DESIGN.md §5); small scenes "

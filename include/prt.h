@@ -119,7 +119,11 @@ int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th
                      uint32_t flags, float* out_sum, uint64_t* stats);
 /* Same work, result left in device memory `d_out_sum` (n_slots x 3 f32) and
  * enqueued on `stream` (a hipStream_t; NULL = the scene's own stream) without
- * a host synchronisation. tile_ids is a host array. */
+ * a host synchronisation. tile_ids is a host array.  The scene keeps one set of
+ * work buffers per stream (up to 8), so renders enqueued on distinct streams may
+ * execute concurrently on the device (e.g. frame k's drain overlapping frame
+ * k+1's start); renders on one stream are ordered as usual.  PRT_FLAG_STATS
+ * counters are shared by all streams. */
 int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw, int th,
                             const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
                             uint32_t flags, float* d_out_sum, void* stream);

@@ -14,6 +14,11 @@ PRT_OK = 0
 PRT_FLAG_STATS = 0x1
 PRT_FLAG_TIME = 0x2
 PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
+# trace-kernel variant ids 1..VAR_LAST (pyrenderer_amd/csrc/prt_kernels.h)
+VAR_LAST = 32
+VAR_WW4_PH_LDS6_DRAIN = 31
+VAR_WW4_Q_SP5_DRAIN = 32
+VAR_WW4_Q_SP5 = 23
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 
@@ -60,6 +65,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB):
             raise PrtError(-100, f"{LIB} not found — run `python -m pyrenderer_amd.build` (hipcc, gfx950)")
+        # torch-ROCm ships its own libamdhip64.so.7 with the same SONAME as /opt/rocm's:
+        # whichever loads first serves the whole process.  Load torch first (when it is
+        # installed) so that libprt and torch share ONE HIP runtime — torch streams and
+        # device pointers handed to libprt are then valid, and torch can still see the GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB)
         for name, (res, args) in EXPORTS.items():
             fn = getattr(L, name)

@@ -14,7 +14,12 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libprt.so")
 SOURCES = ["prt_kernels.hip", "prt_capi.cpp", "prt_bvh.cpp"]
-HEADERS = ["prt_kernels.h", "prt_internal.h"]
+# the persistent trace kernel's instantiation sets: prt_trace_inst.hip compiled once
+# per (traversal stack entries, stats) pair — the objects build in parallel
+TRACE_INST = "prt_trace_inst.hip"
+TRACE_SETS = [(s, t) for s in (4, 10, 16, 32, 64) for t in (0, 1)]
+HEADERS = ["prt_kernels.h", "prt_internal.h", "prt_device.h"]
+OBJ_DIR = os.path.join(LIB_DIR, "obj")
 ARCH = os.environ.get("PRT_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: f32 results must match oracle/prt_oracle.c bit for bit
@@ -22,7 +27,7 @@ ARCH = os.environ.get("PRT_OFFLOAD_ARCH", "gfx950")
 # (hipcc's default -fhip-fp32-correctly-rounded-divide-sqrt).
 # -fno-slp-vectorize: packed-f32 SLP code pins constant pairs in VGPRs (spills at the
 # occupancy targets) and is an anti-lever on CDNA4 (cdna_hip_programming.md, packed f32 VALU).
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize",
          f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 
 
@@ -30,20 +35,42 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "prt.h"), __file__]
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS + [TRACE_INST]] + [os.path.join(ROOT, "include", "prt.h"), __file__]
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
+
+
+def _jobs():
+    n = os.environ.get("MAX_JOBS") or os.cpu_count() or 4
+    return max(1, min(int(n), 16))
 
 
 def build(force=False, verbose=False):
     if not force and not _stale():
         return LIB
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = LIB + ".tmp"
-    cmd = [hipcc] + FLAGS + ["-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
+    units = [(os.path.join(CSRC, f), os.path.join(OBJ_DIR, os.path.splitext(f)[0] + ".o"), []) for f in SOURCES]
+    units += [(os.path.join(CSRC, TRACE_INST), os.path.join(OBJ_DIR, f"prt_trace_{st}_{tt}.o"),
+               [f"-DPRT_STACK={st}", f"-DPRT_STATS={tt}"]) for st, tt in TRACE_SETS]
+    cmds = [[hipcc] + FLAGS + defs + ["-c", src, "-o", obj] for src, obj, defs in units]
     if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd)
+        print(f"compiling {len(cmds)} units with {_jobs()} jobs", flush=True)
+    from concurrent.futures import ThreadPoolExecutor
+    # longest units first (the trace instantiation sets)
+    order = sorted(range(len(cmds)), key=lambda i: TRACE_INST not in cmds[i][-3])
+    with ThreadPoolExecutor(_jobs()) as ex:
+        procs = list(ex.map(lambda i: subprocess.run(cmds[i], capture_output=True, text=True), order))
+    for i, r in zip(order, procs):
+        if r.returncode != 0:
+            sys.stderr.write(" ".join(cmds[i]) + "\n" + r.stdout + r.stderr)
+            raise subprocess.CalledProcessError(r.returncode, cmds[i])
+        if verbose and (r.stderr or r.stdout).strip():
+            print(r.stdout + r.stderr, flush=True)
+    tmp = LIB + ".tmp"
+    link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + [obj for _, obj, _ in units]
+    if verbose:
+        print(" ".join(link), flush=True)
+    subprocess.check_call(link)
     os.replace(tmp, LIB)
     return LIB
 

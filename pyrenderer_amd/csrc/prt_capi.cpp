@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -80,6 +81,18 @@ struct DevBuf {
     void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
 };
 
+// Work buffers of one render stream.  Renders enqueued on distinct streams may run
+// concurrently (a frame's tail overlapping the next frame's start), so everything a
+// launch writes lives here: tile origins, per-sample radiance and primary rays, the
+// work counter + watchdog flag, the spill area and the host-output sums.
+struct RenderCtx {
+    hipStream_t stream = nullptr;
+    DevBuf tiles, buf, rays, work, acc, spill, cont, cont_flag;
+    std::vector<uint32_t> tile_host;
+    uint64_t last_use = 0;
+};
+constexpr size_t kMaxCtx = 8;
+
 struct Scene {
     int device = 0;
     int64_t n_tri = 0;
@@ -94,7 +107,6 @@ struct Scene {
     int n_lt = 0;                    // emitter triangles
     int64_t n_node_f4 = 0, n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
-    DevBuf rays;                     // primary rays of one launch (camera_kernel)
     DevBuf nodes4q;                  // quantised BVH4 (prt_internal.h)
     int64_t n_node4q_f4 = 0;
     DevBuf nodes, nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
@@ -103,13 +115,14 @@ struct Scene {
     int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
     int need4 = 0;                   // worst-case BVH4 traversal stack entries
     int resume_min = 16;             // resume variants (env PRT_RESUME_MIN)
+    int drain_push = 16;             // drain variants (env PRT_DRAIN_PUSH, 0..64)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
-    DevBuf spill;                    // spill variants: deep stack entries
     int64_t n_sph = 0;
-    DevBuf tiles, buf, acc, work, stats;
+    DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
     hipStream_t stream = nullptr;
+    std::vector<std::unique_ptr<RenderCtx>> ctx;  // per render stream (<= kMaxCtx)
+    uint64_t use_clock = 0;
     std::vector<hipEvent_t> ev;   // start/stop pairs of the last timed call
-    std::vector<uint32_t> tile_host;
     int ev_used = 0;
     size_t chunk_bytes = (size_t)4 << 30;  // per-sample buffer budget (HBM is 288 GB)
     size_t device_bytes = 0;
@@ -131,9 +144,13 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->rays, &s->nodes4q, &s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v, &s->light_off, &s->sph, &s->sph_mat,
-                      &s->tiles, &s->buf, &s->acc, &s->work, &s->stats})
+    for (DevBuf* b : {&s->nodes4q, &s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v,
+                      &s->light_off, &s->sph, &s->sph_mat, &s->work, &s->stats})
         b->release();
+    if (!s->ctx.empty()) (void)hipDeviceSynchronize();
+    for (auto& c : s->ctx)
+        for (DevBuf* b : {&c->tiles, &c->buf, &c->rays, &c->work, &c->acc, &c->spill, &c->cont, &c->cont_flag})
+            b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -157,13 +174,50 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
     return PRT_OK;
 }
 
-// work.p: [0] chunk counter; [kFaultOffset] traversal watchdog flag
+constexpr size_t prt_cont_bytes() { return 12 * sizeof(unsigned long long); }  // prt_device.h kContWords
+
+// work.p: [0] chunk counter, [1..3] drain hand-off counters (published, claimed, exited
+// waves); [kFaultOffset] traversal watchdog flag (bit 1: lost hand-off)
 constexpr size_t kFaultOffset = 32;
 
-int read_fault(Scene* s) {
+int read_fault_at(const DevBuf& work) {
     int f = 0;
-    if (hipMemcpy(&f, (char*)s->work.p + kFaultOffset, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (!work.p) return 0;
+    if (hipMemcpy(&f, (char*)work.p + kFaultOffset, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
     return f;
+}
+int read_fault(Scene* s) { return read_fault_at(s->work); }
+// any render context's watchdog flag (callers synchronise first)
+int read_render_faults(Scene* s) {
+    for (auto& c : s->ctx)
+        if (int f = read_fault_at(c->work)) return f;
+    return 0;
+}
+
+// The render context of `stream`, created on first use.  Beyond kMaxCtx streams the
+// least recently used context is recycled after a device synchronisation.
+RenderCtx* ctx_for(Scene* s, hipStream_t stream) {
+    ++s->use_clock;
+    for (auto& c : s->ctx)
+        if (c->stream == stream) { c->last_use = s->use_clock; return c.get(); }
+    if (s->ctx.size() >= kMaxCtx) {
+        auto it = std::min_element(s->ctx.begin(), s->ctx.end(),
+                                   [](const std::unique_ptr<RenderCtx>& a, const std::unique_ptr<RenderCtx>& b) {
+                                       return a->last_use < b->last_use;
+                                   });
+        if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+        (*it)->stream = stream;
+        (*it)->last_use = s->use_clock;
+        return it->get();
+    }
+    auto c = std::unique_ptr<RenderCtx>(new (std::nothrow) RenderCtx());
+    if (!c) return nullptr;
+    if (c->work.ensure(64) != hipSuccess) return nullptr;
+    if (hipMemset(c->work.p, 0, 64) != hipSuccess) return nullptr;
+    c->stream = stream;
+    c->last_use = s->use_clock;
+    s->ctx.push_back(std::move(c));
+    return s->ctx.back().get();
 }
 
 // LDS-resident scene: BVH + triangles small enough to sit beside the stack
@@ -206,17 +260,18 @@ bool camera_is_fast(const float* cam) {
 }
 
 // Enqueue the whole render of a tile set on `stream`, result in d_acc.
-int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids, int n_tiles,
-                   int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc, hipStream_t stream) {
+int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
+                   int n_tiles, int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc) {
     const int64_t n_slots = (int64_t)n_tiles * tw * th;
     if (n_slots == 0) return PRT_OK;
+    hipStream_t stream = cx->stream;
     // per-tile pixel origins (x0 << 16 | y0), staged in a pinned host buffer
     const int tiles_x = (W + tw - 1) / tw;
-    if ((int64_t)s->tile_host.size() < n_tiles) s->tile_host.resize((size_t)n_tiles);
+    if ((int64_t)cx->tile_host.size() < n_tiles) cx->tile_host.resize((size_t)n_tiles);
     for (int i = 0; i < n_tiles; ++i)
-        s->tile_host[(size_t)i] = ((uint32_t)((tile_ids[i] % tiles_x) * tw) << 16) | (uint32_t)((tile_ids[i] / tiles_x) * th);
-    HIP_TRY(s->tiles.ensure(sizeof(uint32_t) * (size_t)n_tiles));
-    HIP_TRY(hipMemcpyAsync(s->tiles.p, s->tile_host.data(), sizeof(uint32_t) * (size_t)n_tiles, hipMemcpyHostToDevice,
+        cx->tile_host[(size_t)i] = ((uint32_t)((tile_ids[i] % tiles_x) * tw) << 16) | (uint32_t)((tile_ids[i] / tiles_x) * th);
+    HIP_TRY(cx->tiles.ensure(sizeof(uint32_t) * (size_t)n_tiles));
+    HIP_TRY(hipMemcpyAsync(cx->tiles.p, cx->tile_host.data(), sizeof(uint32_t) * (size_t)n_tiles, hipMemcpyHostToDevice,
                            stream));
     if (spp == 0 || depth == 0) {
         HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots, stream));
@@ -230,12 +285,12 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)s->chunk_bytes / per_sample_all));
     // keep every chunk's item count below 2^31 (32-bit work counter)
     chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, ((int64_t)1 << 31) / n_slots - 1));
-    HIP_TRY(s->buf.ensure((size_t)(chunk * per_sample)));
-    if (primary) HIP_TRY(s->rays.ensure((size_t)(chunk * n_slots * 16)));
+    HIP_TRY(cx->buf.ensure((size_t)(chunk * per_sample)));
+    if (primary) HIP_TRY(cx->rays.ensure((size_t)(chunk * n_slots * 16)));
     const bool stats = (flags & PRT_FLAG_STATS) != 0;
     const bool timed = (flags & PRT_FLAG_TIME) != 0;
     if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), stream));
-    HIP_TRY(hipMemsetAsync((char*)s->work.p + kFaultOffset, 0, sizeof(int), stream));
+    HIP_TRY(hipMemsetAsync((char*)cx->work.p + kFaultOffset, 0, sizeof(int), stream));
 
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
@@ -252,7 +307,8 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     {
         P.cam_fast = cam_fast ? 1 : 0;
         P.resume_min = s->resume_min;
-        P.rays = primary ? (const float4*)s->rays.p : nullptr;
+        P.drain_push = s->drain_push;
+        P.rays = primary ? (const float4*)cx->rays.p : nullptr;
         const float rd2 = -cam[18];
         for (int i = 0; i < 3; ++i) {
             const float* c = cam + 4 * i;
@@ -264,13 +320,13 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     P.wm1 = (float)(W - 1); P.hm1 = (float)(H - 1);
     P.log_tw = __builtin_ctz((unsigned)tw);
     P.log_tpx = __builtin_ctz((unsigned)(tw * th));
-    P.tile_xy = (const uint32_t*)s->tiles.p;
+    P.tile_xy = (const uint32_t*)cx->tiles.p;
     P.n_slots = (int)n_slots;
     P.depth = depth;
     P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
-    P.work = (uint32_t*)s->work.p;
-    P.fault = (int*)((char*)s->work.p + kFaultOffset);
-    P.out = (float*)s->buf.p;
+    P.work = (uint32_t*)cx->work.p;
+    P.fault = (int*)((char*)cx->work.p + kFaultOffset);
+    P.out = (float*)cx->buf.p;
     P.stats = (unsigned long long*)s->stats.p;
     scene_sizes(s, false, P);
     int stack = s->stack;
@@ -299,10 +355,19 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
     if (spill) {
         // entries [spill_lds, need4] of every lane of the largest grid, plus one slot of headroom
         size_t per_lane = (size_t)std::max(1, s->need4 + 2 - s->spill_lds);
-        HIP_TRY(s->spill.ensure(per_lane * (size_t)occ * s->cus * 256 * sizeof(int)));
-        P.spill = (int*)s->spill.p;
+        HIP_TRY(cx->spill.ensure(per_lane * (size_t)occ * s->cus * 256 * sizeof(int)));
+        P.spill = (int*)cx->spill.p;
     }
 
+    const bool drain = prt::variant_drains(var);
+    const size_t grid_lanes = (size_t)occ * s->cus * 256;
+    if (drain) {
+        // one continuation slot per lane of the largest grid (a path is published at most once)
+        HIP_TRY(cx->cont.ensure(grid_lanes * prt_cont_bytes()));
+        HIP_TRY(cx->cont_flag.ensure(grid_lanes * sizeof(uint32_t)));
+        P.cont = (unsigned long long*)cx->cont.p;
+        P.cont_flag = (uint32_t*)cx->cont_flag.p;
+    }
     int64_t n_chunks = (spp + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
     int k = s->ev_used / 2;
@@ -320,12 +385,13 @@ int enqueue_render(Scene* s, const float* cam, int W, int H, int tw, int th, con
         P.n_items = (uint64_t)(n * n_slots);
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
-        HIP_TRY(hipMemsetAsync(s->work.p, 0, 16, stream));
-        if (primary) HIP_TRY(prt::launch_camera(P, (float4*)s->rays.p, stream));
+        HIP_TRY(hipMemsetAsync(cx->work.p, 0, 16, stream));
+        if (drain) HIP_TRY(hipMemsetAsync(cx->cont_flag.p, 0, sizeof(uint32_t) * (size_t)grid * 256, stream));
+        if (primary) HIP_TRY(prt::launch_camera(P, (float4*)cx->rays.p, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
         HIP_TRY(prt::launch_trace(P, stack, var, grid, stats, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k + 1], stream));
-        HIP_TRY(prt::launch_reduce((const float*)s->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0, stream));
+        HIP_TRY(prt::launch_reduce((const float*)cx->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0, stream));
     }
     return PRT_OK;
 }
@@ -489,6 +555,7 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         s->n_node_f4 = (int64_t)bvh.nodes.size() / 4;
         s->n_tri_f4 = (int64_t)bvh.tris.size() / 4;
         if (const char* rm = std::getenv("PRT_RESUME_MIN")) s->resume_min = std::max(1, std::min(64, std::atoi(rm)));
+        if (const char* dp = std::getenv("PRT_DRAIN_PUSH")) s->drain_push = std::max(0, std::min(64, std::atoi(dp)));
         if (const char* sl = std::getenv("PRT_SPILL_LDS")) {
             int v = std::atoi(sl);
             s->spill_lds = v == 4 ? 4 : v == 32 ? 32 : 16;
@@ -569,14 +636,16 @@ int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th
     if (!out_sum) return fail(PRT_ERR_ARG, "out_sum is NULL");
     DeviceGuard g(s->device);
     const int64_t n_slots = (int64_t)n_tiles * tw * th;
-    HIP_TRY(s->acc.ensure(std::max<size_t>(16, sizeof(float) * 3 * (size_t)n_slots)));
-    if ((rc = enqueue_render(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, (float*)s->acc.p,
-                             s->stream)))
+    RenderCtx* cx = ctx_for(s, s->stream);
+    if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
+    HIP_TRY(cx->acc.ensure(std::max<size_t>(16, sizeof(float) * 3 * (size_t)n_slots)));
+    if ((rc = enqueue_render(s, cx, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, (float*)cx->acc.p)))
         return rc;
     if (n_slots)
-        HIP_TRY(hipMemcpyAsync(out_sum, s->acc.p, sizeof(float) * 3 * (size_t)n_slots, hipMemcpyDeviceToHost, s->stream));
+        HIP_TRY(hipMemcpyAsync(out_sum, cx->acc.p, sizeof(float) * 3 * (size_t)n_slots, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if (read_fault(s) != 0) return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
+    if (read_fault_at(cx->work) != 0)
+        return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     if (stats) {
         if (flags & PRT_FLAG_STATS) {
             unsigned long long h[4];
@@ -597,8 +666,9 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
     if (rc) return rc;
     if (!d_out_sum && n_tiles > 0) return fail(PRT_ERR_ARG, "d_out_sum is NULL");
     DeviceGuard g(s->device);
-    return enqueue_render(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, d_out_sum,
-                          stream ? (hipStream_t)stream : s->stream);
+    RenderCtx* cx = ctx_for(s, stream ? (hipStream_t)stream : s->stream);
+    if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
+    return enqueue_render(s, cx, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, d_out_sum);
 }
 
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
@@ -614,7 +684,7 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
     }
     *ms_total = tot;
     *launches = s->ev_used / 2;
-    if (read_fault(s) != 0) {
+    if (read_render_faults(s) != 0) {
         s->ev_used = 0;
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     }

@@ -16,735 +16,20 @@
 // Closest hit = minimal (t, original triangle index); the BVH only prunes.
 #pragma clang fp contract(off)
 
-#include <hip/hip_runtime.h>
-#include <type_traits>
-#include <stdint.h>
-
-#include "prt_kernels.h"
+#include "prt_device.h"
 
 namespace prt {
+
+// per-(stack, stats) trace-kernel instantiation sets, compiled in parallel from
+// prt_trace_inst.hip (one object each)
+#define PRT_INST_LIST(X) X(4, 0) X(4, 1) X(10, 0) X(10, 1) X(16, 0) X(16, 1) X(32, 0) X(32, 1) X(64, 0) X(64, 1)
+#define PRT_DECL_INST(S, T)                                                                              \
+    hipError_t launch_trace_##S##_##T(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream); \
+    int trace_occ_##S##_##T(int var, size_t smem);
+PRT_INST_LIST(PRT_DECL_INST)
+#undef PRT_DECL_INST
+
 namespace {
-
-constexpr float kInvPi = 0.31830988618379067154f;
-constexpr float kPiOver4 = 0.78539816339744830961f;
-constexpr float kTMin = 0.00001f;    // core/tracing.py:127
-constexpr float kTMax = 99999.9f;    // core/tracing.py:127
-constexpr float kGamma = 0x1.000006p+0f;  // f32(1 + 2*GAMMA2_3), bvh_taichi.py:179
-constexpr int kBlock = 256;
-constexpr int kChunk = 64;           // work items per queue refill (one atomic)
-
-struct V3 { float x, y, z; };
-__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
-__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
-__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ V3 cross(V3 a, V3 b) {
-    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-// a / b is NaN (IEEE): a or b NaN, 0/0 or inf/inf
-__device__ __forceinline__ bool div_is_nan(float a, float b) {
-    return isnan(a) || isnan(b) || (a == 0.0f && b == 0.0f) || (isinf(a) && isinf(b));
-}
-// taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt)
-__device__ __forceinline__ V3 normalize(V3 a) {
-    float l = sqrtf(dot(a, a));
-    return v3(a.x / l, a.y / l, a.z / l);
-}
-__device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
-
-// ------------------------------------------------------------------ RNG spec
-__device__ __forceinline__ uint32_t pcg_permute(uint32_t s) {
-    uint32_t w = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
-    return (w >> 22u) ^ w;
-}
-__device__ __forceinline__ uint32_t pcg_hash(uint32_t v) { return pcg_permute(v * 747796405u + 2891336453u); }
-__device__ __forceinline__ uint32_t rng_key(uint32_t seed_lo, uint32_t seed_hi, uint32_t pixel, uint32_t sample) {
-    uint32_t h = pcg_hash(seed_lo);
-    h = pcg_hash(h ^ seed_hi ^ pixel);
-    return pcg_hash(h + sample);
-}
-__device__ __forceinline__ float rng_next(uint32_t& st) {
-    st = st * 747796405u + 2891336453u;
-    return (float)(pcg_permute(st) >> 8) * 0x1p-24f;
-}
-// taichi_glsl randInt(a, b), inclusive
-__device__ __forceinline__ int rng_int(uint32_t& st, int a, int b) {
-    float u = rng_next(st);
-    int k = (int)floorf(u * (float)(b - a + 1));
-    k = k > b - a ? b - a : k;
-    return a + k;
-}
-
-// --------------------------------------------- concentric disk (samplers.py:9-32)
-__device__ __forceinline__ float poly_sin(float x) {
-    float z = x * x;
-    return ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x + x;
-}
-__device__ __forceinline__ float poly_cos(float x) {
-    float z = x * x;
-    return ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z
-           - 0.5f * z + 1.0f;
-}
-__device__ __forceinline__ V3 cosine_hemisphere(float u0, float u1) {
-    float ox = 2.0f * u0 - 1.0f, oy = 2.0f * u1 - 1.0f;
-    float dx = 0.0f, dy = 0.0f;
-    if (!(ox == 0.0f && oy == 0.0f)) {
-        float r, c, s;
-        if (fabsf(ox) > fabsf(oy)) {
-            r = ox;
-            float th = kPiOver4 * (oy / ox);
-            c = poly_cos(th); s = poly_sin(th);
-        } else {
-            r = oy;
-            float a = kPiOver4 * (ox / oy);   // theta = pi/2 - a
-            c = poly_sin(a); s = poly_cos(a);
-        }
-        dx = r * c; dy = r * s;
-    }
-    float m = 1.0f - dx * dx - dy * dy;
-    return v3(dx, dy, sqrtf(m > 0.0f ? m : 0.0f));
-}
-
-// rotate_z_to + rotate_vector (mat4_taichi.py:9-60): rows (x, z, n)
-__device__ __forceinline__ V3 to_world(V3 n, V3 l) {
-    V3 v = normalize(n);
-    V3 r1, r2, r3;
-    if (v.y == 1.0f) {
-        r1 = v3(1, 0, 0); r2 = v3(0, 0, 1); r3 = v3(0, 1, 0);
-    } else if (v.y == -1.0f) {
-        r1 = v3(1, 0, 0); r2 = v3(0, 0, 1); r3 = v3(0, -1, 0);
-    } else {
-        V3 x = normalize(cross(v, v3(0.0f, 1.0f, 0.0f)));
-        V3 z = normalize(cross(x, v));
-        r1 = x; r2 = z; r3 = v;
-    }
-    return normalize(r1 * l.x + r2 * l.y + r3 * l.z);
-}
-
-// ------------------------------------------------------- camera (camera_taichi.py:47-74)
-__device__ __forceinline__ void gen_ray(const float* cam, float u, float v, uint32_t& st, V3& o, V3& d) {
-    const float sd0 = cam[16], sd1 = cam[17], sd2 = cam[18], sd3 = cam[19];
-    float rd[4] = {(u - 0.5f) * sd0 / 0.5f, (v - 0.5f) * sd1 / 0.5f, -sd2, 1.0f};
-    float ro[4] = {0.0f, 0.0f, 0.0f, 1.0f};
-    if (sd3 > 0.0f) {
-        ro[0] = sd2 * rng_next(st) - sd2 / 2.0f;
-        ro[1] = sd2 * rng_next(st) - sd2 / 2.0f;
-    }
-    float dw[4], ow[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float* c = cam + 4 * i;
-        dw[i] = rd[0] * c[0] + rd[1] * c[1] + rd[2] * c[2] + rd[3] * c[3];
-        ow[i] = ro[0] * c[0] + ro[1] * c[1] + ro[2] * c[2] + ro[3] * c[3];
-    }
-    float f0 = dw[0] - ow[0], f1 = dw[1] - ow[1], f2 = dw[2] - ow[2], f3 = dw[3] - ow[3];
-    float l = sqrtf(f0 * f0 + f1 * f1 + f2 * f2 + f3 * f3);
-    o = v3(ow[0], ow[1], ow[2]);
-    d = v3(f0 / l, f1 / l, f2 / l);
-}
-
-// -------------------------------------- specular helpers (bsdf_taichi.py:6-22)
-__device__ __forceinline__ float schlick(float cosine, float idx) {
-    float r0 = (1.0f - idx) / (1.0f + idx);
-    r0 = r0 * r0;
-    float m = 1.0f - cosine;
-    return r0 + (1.0f - r0) * (m * m * m * m * m);
-}
-__device__ __forceinline__ V3 reflect3(V3 v, V3 n) { return v - n * (2.0f * dot(v, n)); }
-__device__ __forceinline__ V3 refract3(V3 v, V3 n, float eta) {
-    float ct = -dot(v, n);
-    ct = ct > 1.0f ? 1.0f : ct;
-    V3 perp = (v + n * ct) * eta;
-    float k = 1.0f - dot(perp, perp);
-    return perp + n * (-sqrtf(fabsf(k)));
-}
-// random_in_unit_sphere (vec3_taichi.py:299-306) with deterministic ops: see oracle
-__device__ __forceinline__ float cbrt_spec(float x) {
-    if (!(x > 0.0f)) return 0.0f;
-    float y = __uint_as_float(__float_as_uint(x) / 3u + 709921077u);
-    for (int i = 0; i < 3; ++i) y = (2.0f * y + x / (y * y)) / 3.0f;
-    return y;
-}
-__device__ __forceinline__ V3 random_in_unit_sphere(uint32_t& st) {
-    float u1 = rng_next(st), u2 = rng_next(st), u3 = rng_next(st);
-    int q = (int)floorf(u1 * 4.0f + 0.5f);
-    float a = 6.28318530717958647692f * (u1 - 0.25f * (float)q);
-    float pc = poly_cos(a), ps = poly_sin(a);
-    float c, sn;
-    switch (q & 3) {
-        case 0: c = pc; sn = ps; break;
-        case 1: c = -ps; sn = pc; break;
-        case 2: c = -pc; sn = -ps; break;
-        default: c = ps; sn = -pc; break;
-    }
-    float z = 2.0f * u2 - 1.0f;
-    float m = 1.0f - z * z;
-    float sp = sqrtf(m > 0.0f ? m : 0.0f);
-    float r = cbrt_spec(u3);
-    return v3(r * sp * c, r * sp * sn, r * z);
-}
-// hit_sphere (intersection_taichi.py:15-36): nearest root in [t_min, t_max], else far root
-__device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, float t_max, float& root) {
-    V3 oc = o - xyz(sc);
-    float a = dot(d, d);
-    float half_b = dot(oc, d);
-    float cc = dot(oc, oc) - sc.w * sc.w;
-    float disc = half_b * half_b - a * cc;
-    if (!(disc >= 0.0f)) return false;
-    float sq = sqrtf(disc);
-    root = (-half_b - sq) / a;
-    if (root < t_min || t_max < root) {
-        root = (-half_b + sq) / a;
-        if (root < t_min || t_max < root) return false;
-    }
-    return true;
-}
-
-// ---------------------------------------------------------------- traversal
-struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp; };
-
-// Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
-// t = (lo - o) / d is evaluated as fma(lo, 1/d, -o/d): pruning only, so the few-ulp
-// error of the estimate is covered by the box padding (~1e-6 of the scene scale,
-// >> |o/d| ulp) and the 1+2*gamma3 factor on t_far.  The near and far plane of each
-// axis are chosen by the sign of 1/d, NOT by min/max of the two distances: for a
-// direction component of exactly 0 (1/d = inf) a plane distance can be NaN, and
-// fminf/fmaxf would then turn the other plane's -inf into the FAR distance and cull
-// a box the ray lies inside (measured: 8 of 262144 pixels at config 2).  With the
-// selection, a NaN distance is dropped by the fmaxf/fminf that follow, which can
-// only enlarge the interval.  sx/sy/sz: 1/d.{x,y,z} < 0.
-__device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 oi, V3 inv,
-                                     float tmin, float tmax, float& tn) {
-    const bool sx = __float_as_int(inv.x) < 0, sy = __float_as_int(inv.y) < 0, sz = __float_as_int(inv.z) < 0;
-    float ax = __builtin_fmaf(lx, inv.x, -oi.x), bx = __builtin_fmaf(hx, inv.x, -oi.x);
-    float ay = __builtin_fmaf(ly, inv.y, -oi.y), by = __builtin_fmaf(hy, inv.y, -oi.y);
-    float az = __builtin_fmaf(lz, inv.z, -oi.z), bz = __builtin_fmaf(hz, inv.z, -oi.z);
-    float nx = sx ? bx : ax, fx = sx ? ax : bx;
-    float ny = sy ? by : ay, fy = sy ? ay : by;
-    float nz = sz ? bz : az, fz = sz ? az : bz;
-    float tnear = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
-    float tfar = fminf(fminf(fx, fy), fminf(fz, tmax)) * kGamma;   // min(a g, b g) = min(a, b) g (g > 0)
-    tn = tnear;
-    return tnear <= tfar;
-}
-
-// Moller-Trumbore in the reference's exact expression order
-// (intersection_taichi.py:69-91).  `accept(t)` decides the t-range part.
-template <bool ANY>
-__device__ __forceinline__ bool mt(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, float tbest, int id, int best_id,
-                                   float& tout) {
-    V3 c = cross(e1, d);
-    float det = dot(c, e2);
-    if (!(fabsf(det) > 0.0f)) return false;
-    float f = 1.0f / det;
-    V3 s = o - v0;
-    V3 q = cross(s, e2);
-    float t = -f * dot(q, e1);
-    bool in_range = ANY ? (t0 < t && t < tbest) : (t0 < t && (t < tbest || (t == tbest && id < best_id)));
-    if (!in_range) return false;
-    float u = -f * dot(q, d);
-    if (!(0.0f <= u && u <= 1.0f)) return false;
-    float v = f * dot(c, s);
-    if (!(v >= 0.0f && 1.0f - u - v >= 0.0f)) return false;
-    tout = t;
-    return true;
-}
-
-// Closest hit (ANY=false) or any hit (ANY=true) over the BVH2.
-// lstack: this lane's LDS stack, entry k at lstack[k * kBlock].
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool traverse(const TraceParams& P, V3 o, V3 d, float tmin, float tmax, int* lstack,
-                                         int& hit_id, float& hit_t, Counters& cn) {
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    V3 oi = o * inv;
-    float best = tmax;
-    int best_id = -1;
-    int sp = 0;
-    int cur = 0;
-    while (true) {
-        if (cur >= 0) {
-            const float4* nd = P.nodes + (size_t)cur * 4;
-            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            if (STATS) cn.nodes++;
-            float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
-            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
-            if (hl && hr) {
-                bool lf = tl <= tr;
-                cur = lf ? cl : cr;
-                lstack[sp * kBlock] = lf ? cr : cl;
-                ++sp;
-            } else if (hl) {
-                cur = cl;
-            } else if (hr) {
-                cur = cr;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                cur = lstack[sp * kBlock];
-            }
-        } else {
-            int v = -cur - 1;
-            int first = v >> 3, cnt = (v & 7) + 1;
-            for (int k = 0; k < cnt; ++k) {
-                const float4* tp = P.tris + (size_t)(first + k) * 3;
-                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
-                int id = __float_as_int(t0.w);
-                float t;
-                if (STATS) cn.tris++;
-                if (mt<ANY>(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, t)) {
-                    best = t;
-                    best_id = id;
-                    if (ANY) { hit_id = id; hit_t = t; return true; }
-                }
-            }
-            if (sp == 0) break;
-            --sp;
-            cur = lstack[sp * kBlock];
-        }
-    }
-    hit_id = best_id;
-    hit_t = best;
-    return best_id >= 0;
-}
-
-// Unified traversal: one loop serves closest-hit (extension) and any-hit
-// (shadow) lanes of the same wave, so the two query kinds never serialise.
-// nodes/tris point either to global memory or to the block's LDS copy of a
-// small scene (the compiler infers the address space after inlining).
-__device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, float tbest, int id, int best_id,
-                                     bool any, float& tout) {
-    V3 c = cross(e1, d);
-    float det = dot(c, e2);
-    if (!(fabsf(det) > 0.0f)) return false;
-    float f = 1.0f / det;
-    V3 s = o - v0;
-    V3 q = cross(s, e2);
-    float t = -f * dot(q, e1);
-    bool in_range = t0 < t && (t < tbest || (!any && t == tbest && id < best_id));
-    if (!in_range) return false;
-    float u = -f * dot(q, d);
-    if (!(0.0f <= u && u <= 1.0f)) return false;
-    float v = f * dot(c, s);
-    if (!(v >= 0.0f && 1.0f - u - v >= 0.0f)) return false;
-    tout = t;
-    return true;
-}
-
-template <bool STATS>
-__device__ __forceinline__ bool traverse_u(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                           V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
-                                           float& hit_t, Counters& cn) {
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    V3 oi = o * inv;
-    float best = tmax;
-    int best_id = -1;
-    int sp = 0;
-    int cur = 0;
-    while (true) {
-        if (cur >= 0) {
-            const float4* nd = nodes + (size_t)cur * 4;
-            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            if (STATS) cn.nodes++;
-            float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
-            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
-            if (hl && hr) {
-                bool lf = tl <= tr;
-                cur = lf ? cl : cr;
-                lstack[sp * kBlock] = lf ? cr : cl;
-                ++sp;
-            } else if (hl | hr) {
-                cur = hl ? cl : cr;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                cur = lstack[sp * kBlock];
-            }
-        } else {
-            int v = -cur - 1;
-            int first = v >> 3, cnt = (v & 7) + 1;
-            bool done = false;
-            for (int k = 0; k < cnt; ++k) {
-                const float4* tp = tris + (size_t)(first + k) * 3;
-                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
-                int id = __float_as_int(t0.w);
-                float t;
-                if (STATS) cn.tris++;
-                if (mt_u(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, any, t)) {
-                    best = t;
-                    best_id = id;
-                    if (any) { done = true; break; }
-                }
-            }
-            if (done || sp == 0) break;
-            --sp;
-            cur = lstack[sp * kBlock];
-        }
-    }
-    hit_id = best_id;
-    hit_t = best;
-    return best_id >= 0;
-}
-
-// While-while traversal (Aila & Laine 2009, "persistent while-while"): lanes
-// descend inner nodes until every lane of the wave holds a postponed leaf,
-// then all lanes test leaf triangles together, so inner-node and leaf work
-// of different lanes do not serialise against each other.  Stack bottom
-// holds kSentinel; leaves are negative references, inner nodes >= 0.
-constexpr int kSentinel = 0x7FFFFFFF;
-constexpr uint32_t kGuardTrips = 1u << 20;   // leaf batches per query before the watchdog trips
-
-template <bool STATS>
-__device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                            V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
-                                            float& hit_t, Counters& cn) {
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    V3 oi = o * inv;
-    float best = tmax;
-    int best_id = -1;
-    lstack[0] = kSentinel;
-    int sp = 0;         // index of the top entry
-    int cur = 0;        // root
-    int leaf = 0;       // postponed leaf (< 0); >= 0 means none
-    do {
-        // --- inner nodes until all lanes have a postponed leaf
-        while (cur >= 0 && cur != kSentinel) {
-            const float4* nd = nodes + (size_t)cur * 4;
-            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            if (STATS) { cn.nodes++; cn.it_inner++; }
-            float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
-            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
-            if (!hl && !hr) {
-                cur = lstack[sp * kBlock];
-                --sp;
-            } else {
-                bool lf = hl && (!hr || tl <= tr);
-                cur = lf ? cl : cr;
-                if (hl && hr) {
-                    ++sp;
-                    lstack[sp * kBlock] = lf ? cr : cl;
-                }
-            }
-            if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
-                leaf = cur;
-                cur = lstack[sp * kBlock];
-                --sp;
-            }
-            if (!__any(leaf >= 0)) break;  // every lane holds a leaf: go test triangles
-        }
-        // --- leaves
-        while (leaf < 0) {
-            int v = -leaf - 1;
-            int first = v >> 3, cnt = (v & 7) + 1;
-            if (STATS) cn.it_leaf++;
-            for (int k = 0; k < cnt; ++k) {
-                const float4* tp = tris + (size_t)(first + k) * 3;
-                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
-                int id = __float_as_int(t0.w);
-                float t;
-                if (STATS) cn.tris++;
-                if (mt_u(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, any, t)) {
-                    best = t;
-                    best_id = id;
-                    if (any) { cur = kSentinel; break; }
-                }
-            }
-            if (any && best_id >= 0) { leaf = 0; break; }
-            leaf = cur;
-            if (cur < 0) {
-                cur = lstack[sp * kBlock];
-                --sp;
-            }
-        }
-    } while (cur != kSentinel || leaf < 0);
-    hit_id = best_id;
-    hit_t = best;
-    return best_id >= 0;
-}
-
-// While-while over the BVH4 (prt_internal.h): one node fetch tests four child
-// boxes; hit children are ordered near-to-far with a 5-comparator network, the
-// nearest is visited next and the others pushed far-first.
-__device__ __forceinline__ void cswap(float& ta, int& ra, float& tb, int& rb) {
-    bool sw = tb < ta;
-    float t = sw ? tb : ta;
-    tb = sw ? ta : tb;
-    ta = t;
-    int r = sw ? rb : ra;
-    rb = sw ? ra : rb;
-    ra = r;
-}
-
-// Per-lane traversal stacks.  LdsStack: entry k at l[k * kBlock] (conflict-free).
-// SpillStack: the first LST entries in LDS, deeper ones in a per-lane global area
-// (stride = all threads of the grid); deep stacks are rare (max 24 entries measured on
-// the 1 M-triangle scene against a worst-case bound of 46), so a small LDS stack keeps
-// occupancy and the spill branch is almost never taken.
-struct LdsStack {
-    int* l;
-    __device__ __forceinline__ void put(int k, int v) { l[k * kBlock] = v; }
-    __device__ __forceinline__ int get(int k) const { return l[k * kBlock]; }
-};
-template <int LST>
-struct SpillStack {
-    int* l;
-    int* g;
-    uint32_t gs;
-    __device__ __forceinline__ void put(int k, int v) {
-        if (k < LST) l[k * kBlock] = v;
-        else g[(size_t)(k - LST) * gs] = v;
-    }
-    __device__ __forceinline__ int get(int k) const { return k < LST ? l[k * kBlock] : g[(size_t)(k - LST) * gs]; }
-};
-
-// MODE 0: per-lane query kind (`any` may differ between lanes); 1: every lane
-// closest-hit; 2: every lane any-hit (phase-aligned shadow iterations).  Any-hit
-// queries need no visiting order, so mode 2 skips the sorting network.
-// Pushes write the slot above the top unconditionally and advance the stack
-// pointer by the hit predicate (no exec-mask branches); the highest slot written
-// is the same as with conditional pushes (<= 3 above the entry top).
-// Slab test from plane distances already ordered near/far (quantised nodes).
-__device__ __forceinline__ bool slab_t(float nx, float fx, float ny, float fy, float nz, float fz, float tmin,
-                                       float tmax, float& tn) {
-    float tnear = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
-    float tfar = fminf(fminf(fx, fy), fminf(fz, tmax)) * kGamma;
-    tn = tnear;
-    return tnear <= tfar;
-}
-__device__ __forceinline__ float ubyte(uint32_t w, int k) {
-    return (float)((w >> (8 * k)) & 0xFFu);   // v_cvt_f32_ubyte{k}
-}
-// Child k of a quantised node (prt_internal.h): plane distance (origin + q s - o) / d
-// evaluated as fma(q, s/d, (origin - o)/d); the >= 2 pad outward rounding of the grid
-// covers the estimate's error, so the test stays conservative.  The q words arrive
-// already swapped into near/far order by the sign of 1/d (see slab()).
-struct QAxis { float A, B; };
-__device__ __forceinline__ bool qchild(int k, uint32_t lxq, uint32_t hxq, uint32_t lyq, uint32_t hyq, uint32_t lzq,
-                                       uint32_t hzq, QAxis X, QAxis Y, QAxis Z, float tmin, float tmax, float& tn) {
-    return slab_t(__builtin_fmaf(ubyte(lxq, k), X.A, X.B), __builtin_fmaf(ubyte(hxq, k), X.A, X.B),
-                  __builtin_fmaf(ubyte(lyq, k), Y.A, Y.B), __builtin_fmaf(ubyte(hyq, k), Y.A, Y.B),
-                  __builtin_fmaf(ubyte(lzq, k), Z.A, Z.B), __builtin_fmaf(ubyte(hzq, k), Z.A, Z.B), tmin, tmax, tn);
-}
-
-// Traversal state of a query that may be suspended between loop iterations (RES).
-struct TState { int cur, leaf, sp, best_id; float best; };
-template <class S>
-__device__ __forceinline__ void tstate_init(TState& ts, S stk, float tmax) {
-    stk.put(0, kSentinel);
-    ts.cur = 0; ts.leaf = 0; ts.sp = 0; ts.best_id = -1; ts.best = tmax;
-}
-
-// RES: the wave leaves the traversal loop once fewer than `min_lanes` lanes are still
-// traversing; the unfinished lanes keep their state (registers + LDS stack) and resume
-// in the next iteration, so the long tail of a few slow lanes no longer idles the
-// others.  Returns whether the query finished (hit_id / hit_t valid).
-// Slab test with the near/far planes already selected by the sign of 1/d (BVH4
-// nodes: the selection is an address offset, no per-plane selects); same values as
-// slab().
-__device__ __forceinline__ bool slab_nf(float nx, float fx, float ny, float fy, float nz, float fz, V3 oi, V3 inv,
-                                        float tmin, float tmax, float& tn) {
-    float ax = __builtin_fmaf(nx, inv.x, -oi.x), bx = __builtin_fmaf(fx, inv.x, -oi.x);
-    float ay = __builtin_fmaf(ny, inv.y, -oi.y), by = __builtin_fmaf(fy, inv.y, -oi.y);
-    float az = __builtin_fmaf(nz, inv.z, -oi.z), bz = __builtin_fmaf(fz, inv.z, -oi.z);
-    float tnear = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin));
-    float tfar = fminf(fminf(bx, by), fminf(bz, tmax)) * kGamma;
-    tn = tnear;
-    return tnear <= tfar;
-}
-
-template <bool STATS, int MODE, class S, bool QN = false, bool RES = false>
-__device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                             V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
-                                             float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0,
-                                             int* fault = nullptr) {
-    const bool any = MODE == 0 ? any_lane : MODE == 2;
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    V3 oi = o * inv;
-    // near plane index per axis (0 = lo, 1 = hi) from the sign of 1/d
-    const int sx = __float_as_int(inv.x) < 0 ? 1 : 0, sy = __float_as_int(inv.y) < 0 ? 1 : 0,
-              sz = __float_as_int(inv.z) < 0 ? 1 : 0;
-    TState ts;
-    if (RES) ts = *tsp;
-    else tstate_init(ts, stk, tmax);
-    float best = ts.best;
-    int best_id = ts.best_id;
-    uint32_t guard = 0;
-    int sp = ts.sp;
-    int cur = ts.cur;
-    int leaf = ts.leaf;
-    do {
-        while (cur >= 0 && cur != kSentinel) {
-            float t0, t1, t2, t3;
-            bool h0, h1, h2, h3;
-            int r0, r1, r2, r3;
-            if (QN) {
-                const float4* nd = nodes + (size_t)cur * 4;
-                float4 a = nd[0], b = nd[1], c = nd[2], rf = nd[3];
-                if (STATS) { cn.nodes++; cn.it_inner++; }
-                QAxis X = {a.w * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
-                QAxis Y = {b.x * inv.y, __builtin_fmaf(a.y, inv.y, -oi.y)};
-                QAxis Z = {b.y * inv.z, __builtin_fmaf(a.z, inv.z, -oi.z)};
-                uint32_t lxq = __float_as_uint(sx ? b.w : b.z), hxq = __float_as_uint(sx ? b.z : b.w);
-                uint32_t lyq = __float_as_uint(sy ? c.y : c.x), hyq = __float_as_uint(sy ? c.x : c.y);
-                uint32_t lzq = __float_as_uint(sz ? c.w : c.z), hzq = __float_as_uint(sz ? c.z : c.w);
-                r0 = __float_as_int(rf.x); r1 = __float_as_int(rf.y); r2 = __float_as_int(rf.z); r3 = __float_as_int(rf.w);
-                h0 = qchild(0, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t0) && r0 != kSentinel;
-                h1 = qchild(1, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t1) && r1 != kSentinel;
-                h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && r2 != kSentinel;
-                h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && r3 != kSentinel;
-            } else {
-                // near/far planes picked by address (the node stores lo and hi per axis)
-                const float4* nd = nodes + (size_t)cur * 8;
-                float4 nx = nd[sx], fx = nd[1 - sx], ny = nd[2 + sy], fy = nd[3 - sy], nz = nd[4 + sz], fz = nd[5 - sz];
-                float4 rf = nd[6];
-                if (STATS) { cn.nodes++; cn.it_inner++; }
-                h0 = slab_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, oi, inv, tmin, best, t0);
-                h1 = slab_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, oi, inv, tmin, best, t1);
-                h2 = slab_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, oi, inv, tmin, best, t2);
-                h3 = slab_nf(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, oi, inv, tmin, best, t3);
-                r0 = __float_as_int(rf.x); r1 = __float_as_int(rf.y); r2 = __float_as_int(rf.z); r3 = __float_as_int(rf.w);
-            }
-            if (MODE == 2) {
-                stk.put(sp + 1, r0); sp += h0 ? 1 : 0;
-                stk.put(sp + 1, r1); sp += h1 ? 1 : 0;
-                stk.put(sp + 1, r2); sp += h2 ? 1 : 0;
-                int top = stk.get(sp);
-                cur = h3 ? r3 : top;
-                sp -= h3 ? 0 : 1;
-            } else {
-                t0 = h0 ? t0 : INFINITY;
-                t1 = h1 ? t1 : INFINITY;
-                t2 = h2 ? t2 : INFINITY;
-                t3 = h3 ? t3 : INFINITY;
-                int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
-                // nearest hit child first (3 comparators); the other hits pushed in slot order
-                cswap(t0, r0, t1, r1);
-                cswap(t2, r2, t3, r3);
-                cswap(t0, r0, t2, r2);
-                stk.put(sp + 1, r3); sp += t3 != INFINITY ? 1 : 0;
-                stk.put(sp + 1, r2); sp += t2 != INFINITY ? 1 : 0;
-                stk.put(sp + 1, r1); sp += t1 != INFINITY ? 1 : 0;
-                int top = stk.get(sp);
-                cur = nh > 0 ? r0 : top;
-                sp -= nh > 0 ? 0 : 1;
-            }
-            if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
-            if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
-                leaf = cur;
-                cur = stk.get(sp);
-                --sp;
-            }
-            if (!__any(leaf >= 0)) break;
-        }
-        while (leaf < 0) {
-            int v = -leaf - 1;
-            int first = v >> 3, cnt = (v & 7) + 1;
-            if (STATS) cn.it_leaf++;
-            for (int k = 0; k < cnt; ++k) {
-                const float4* tp = tris + (size_t)(first + k) * 3;
-                float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
-                int id = __float_as_int(q0.w);
-                float t;
-                if (STATS) cn.tris++;
-                if (mt_u(xyz(q0), xyz(q1), xyz(q2), o, d, tmin, best, id, best_id, any, t)) {
-                    best = t;
-                    best_id = id;
-                    if (any) { cur = kSentinel; break; }
-                }
-            }
-            if (any && best_id >= 0) { leaf = 0; break; }
-            leaf = cur;
-            if (cur < 0) {
-                cur = stk.get(sp);
-                --sp;
-            }
-        }
-        if (RES && (cur != kSentinel || leaf < 0) && __popcll(__ballot(true)) < min_lanes) break;
-        // watchdog: a traversal revisiting nodes forever (corrupt tree) ends the query and
-        // raises the fault flag that the host turns into an error, instead of hanging the GPU
-        if (++guard > kGuardTrips) {
-            if (fault) atomicOr(fault, 1);
-            cur = kSentinel;
-            leaf = 0;
-        }
-    } while (cur != kSentinel || leaf < 0);
-    hit_id = best_id;
-    hit_t = best;
-    if (RES) {
-        tsp->cur = cur; tsp->leaf = leaf; tsp->sp = sp; tsp->best_id = best_id; tsp->best = best;
-        return !(cur != kSentinel || leaf < 0);
-    }
-    return best_id >= 0;
-}
-
-// Pixel of work item `item` (slot = tile-major, row, column); xy0 = the item's
-// tile origin (x0 << 16 | y0).  Uniform inputs are laundered through SGPR asm so
-// the compiler cannot hoist their VALU-derived values out of the persistent loop
-// (they would pin VGPRs).
-__device__ __forceinline__ void pixel_of(const TraceParams& P, uint32_t item, uint32_t chunk_s, uint32_t xy0, int& x,
-                                         int& y) {
-    int log_tw = P.log_tw, log_tpx = P.log_tpx;
-    asm volatile("" : "+s"(log_tw), "+s"(log_tpx));
-    uint32_t slot = item - chunk_s * (uint32_t)P.n_slots;
-    uint32_t loc = slot & ((1u << log_tpx) - 1u);
-    x = (int)(xy0 >> 16) + (int)(loc & ((1u << log_tw) - 1u));
-    y = (int)(xy0 & 0xFFFFu) + (int)(loc >> log_tw);
-}
-
-// Camera sample for pixel (x, y) of sample `chunk_s` (main_taichi.py:89-95): RNG key,
-// jitter, gen_ray.
-__device__ __forceinline__ void camera_ray(const TraceParams& P, int x, int y, uint32_t chunk_s, uint32_t& st, V3& o,
-                                           V3& d) {
-    int W = P.W;
-    float wm1 = P.wm1, hm1 = P.hm1;
-    asm volatile("" : "+s"(W), "+s"(wm1), "+s"(hm1));
-    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)W + (uint32_t)x, (uint32_t)P.s0 + chunk_s);
-    float r0 = rng_next(st);
-    float u = ((float)x + r0) / wm1;
-    float r1 = rng_next(st);
-    float vv = ((float)y + r1) / hm1;
-    if (P.cam_fast) {
-        // gen_ray for a pinhole affine camera: the same operations minus
-        // those with exactly known results (see TraceParams::cam_fast)
-        float c[12], k[6];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-            c[i] = P.cam[i];
-            asm volatile("" : "+s"(c[i]));
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            k[i] = P.cam_o[i];
-            k[3 + i] = P.cam_k[i];
-            asm volatile("" : "+s"(k[i]), "+s"(k[3 + i]));
-        }
-        float sd0 = P.cam[16], sd1 = P.cam[17];
-        asm volatile("" : "+s"(sd0), "+s"(sd1));
-        float rx = (u - 0.5f) * sd0 / 0.5f, ry = (vv - 0.5f) * sd1 / 0.5f;
-        float f[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) f[i] = (((rx * c[4 * i] + ry * c[4 * i + 1]) + k[3 + i]) + c[4 * i + 3]) - k[i];
-        float ln = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
-        o = v3(k[0], k[1], k[2]);
-        d = v3(f[0] / ln, f[1] / ln, f[2] / ln);
-    } else {
-        float cam[24];
-#pragma unroll
-        for (int i = 0; i < 20; ++i) {
-            cam[i] = P.cam[i];
-            asm volatile("" : "+s"(cam[i]));
-        }
-        gen_ray(cam, u, vv, st, o, d);
-    }
-}
 
 // Primary rays of one launch, generated with every lane busy (the persistent
 // trace kernel would otherwise run this code with the few lanes it refills):
@@ -763,431 +48,6 @@ __global__ __launch_bounds__(kBlock) void camera_kernel(TraceParams P, float4* _
     V3 o, d;
     camera_ray(P, x, y, cs, st, o, d);
     rays[item] = make_float4(d.x, d.y, d.z, __uint_as_float(st));
-}
-
-enum : int { Q_EXT = 0, Q_SHADOW = 1 };
-
-template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
-__global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
-void trace_kernel(TraceParams P) {
-    // VAR = traversal kind (0 split, 1 unified, 2 while-while BVH2, 3 while-while BVH4,
-    // 4 BVH4 + parked state) | 8 for phase-aligned scheduling (see below)
-    constexpr int TRAV = VAR & 7;
-    constexpr bool PHASE = (VAR & 8) != 0;
-    constexpr bool SPILL = (VAR & 32) != 0;    // LDS stack of STACK entries + global spill area
-    constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
-    constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
-    extern __shared__ float4 smem[];
-    constexpr int kStackWords = STACK;
-    // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
-    // while the lane traverses, so traversal registers do not add to it.
-    constexpr int kParkF4 = (TRAV == 4) ? 3 * kBlock : 0;
-    int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
-    using StackT = typename std::conditional<SPILL, SpillStack<STACK>, LdsStack>::type;
-    StackT stk;
-    stk.l = lstack;
-    if constexpr (SPILL) {
-        stk.g = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
-        stk.gs = gridDim.x * kBlock;
-    }
-    float4* park = smem + kStackWords * kBlock / 4 + threadIdx.x;
-    const float4* g_nodes = P.nodes;
-    const float4* g_tris = P.tris;
-    const float4* s_nm = P.tri_nm;
-    const float4* s_fr = P.tri_frame;
-    const float* s_mats = P.mats;
-    const float4* s_lv = P.light_v;
-    const int* s_loff = P.light_off;
-    if (SCENE_LDS) {
-        // small scene: copy BVH + triangles, and the shading data (normals, frames,
-        // materials, emitters), into LDS once per persistent block
-        float4* sn = smem + kStackWords * kBlock / 4 + kParkF4;
-        float4* st4 = sn + P.n_node_f4;
-        float4* snm = st4 + P.n_tri_f4;
-        float4* sfr = snm + P.n_tri;
-        float4* smt = sfr + 6 * P.n_tri;
-        float4* slv = smt + 2 * P.n_mat;
-        int* slo = reinterpret_cast<int*>(slv + 4 * P.n_lt);
-        for (int i = threadIdx.x; i < P.n_node_f4; i += kBlock) sn[i] = P.nodes[i];
-        for (int i = threadIdx.x; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
-        for (int i = threadIdx.x; i < P.n_tri; i += kBlock) snm[i] = P.tri_nm[i];
-        for (int i = threadIdx.x; i < 6 * P.n_tri; i += kBlock) sfr[i] = P.tri_frame[i];
-        for (int i = threadIdx.x; i < 2 * P.n_mat; i += kBlock) smt[i] = reinterpret_cast<const float4*>(P.mats)[i];
-        for (int i = threadIdx.x; i < 4 * P.n_lt; i += kBlock) slv[i] = P.light_v[i];
-        for (int i = threadIdx.x; i <= P.n_light; i += kBlock) slo[i] = P.light_off[i];
-        __syncthreads();
-        g_nodes = sn;
-        g_tris = st4;
-        s_nm = snm;
-        s_fr = sfr;
-        s_mats = reinterpret_cast<const float*>(smt);
-        s_lv = slv;
-        s_loff = slo;
-    }
-    const int lane = threadIdx.x & 63;
-
-    // wave-uniform work queue [q_next, q_end)
-    uint32_t q_next = 0, q_end = 0;
-    bool exhausted = false;
-
-    // lane state
-    TState tst = {0, 0, 0, -1, 0.0f};
-    bool pending = false;   // RESUME: a suspended query (state in tst + the LDS stack)
-    int item = -1;
-    int bounce = 0, qtype = Q_EXT;
-    uint32_t st = 0;
-    V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
-    V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
-    float tmax = kTMax;
-    Counters cn = {0, 0, 0, 0, 0, 0, 0};
-    uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
-    uint32_t chunk_s = 0;   // wave-uniform: sample index (within the launch) of the current chunk
-    uint32_t chunk_xy0 = 0; // wave-uniform: origin of the current chunk's tile
-
-    // diagnostic (STATS) wave-level clocks: refill / traversal / shading, iterations, active lanes
-    uint64_t c_refill = 0, c_trav = 0, c_shade = 0, n_iter = 0, n_active = 0;
-    uint64_t t_a = 0, t_b = 0;
-    // PHASE: the wave alternates extension and shadow iterations, so the costly
-    // shading code (run after extension queries only) and the refill execute
-    // with every busy lane at once instead of every iteration with about half.
-    // Lanes whose query kind does not match the wave's phase sit the iteration out.
-    bool last_shadow = false;
-    while (true) {
-        if (STATS) t_a = __builtin_amdgcn_s_memtime();
-        bool do_shadow = false;
-        if (PHASE) {
-            do_shadow = !last_shadow && __ballot(item >= 0 && qtype == Q_SHADOW) != 0;
-            last_shadow = do_shadow;
-        }
-        // ---------------------------------------------------------- refill
-        uint64_t idle = do_shadow ? 0ull : __ballot(item < 0);
-        for (int round = 0; round < 2 && idle; ++round) {
-            uint32_t avail = q_end - q_next;
-            if (avail == 0 && !exhausted) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(P.work, (uint32_t)kChunk);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if ((uint64_t)base >= P.n_items) {
-                    exhausted = true;
-                } else {
-                    q_next = base;
-                    q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
-                    // n_slots is a multiple of 64 (tile sizes are powers of two >= 64 px),
-                    // so a chunk never straddles two samples: one scalar division per chunk
-                    chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
-                    // tiles hold >= 64 pixels (powers of two), so the chunk lies in one tile
-                    uint32_t tk = (base - chunk_s * (uint32_t)P.n_slots) >> P.log_tpx;
-                    chunk_xy0 = __builtin_amdgcn_readfirstlane(P.tile_xy[tk]);
-                }
-                avail = q_end - q_next;
-            }
-            if (avail == 0) break;
-            uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-            uint32_t need = (uint32_t)__popcll(idle);
-            uint32_t take = need < avail ? need : avail;
-            if (((idle >> lane) & 1ull) && rank < take) {
-                item = (int)(q_next + rank);
-                // start a new sample: main_taichi.py:89-95
-                L = v3(0, 0, 0);
-                int x, y;
-                pixel_of(P, (uint32_t)item, chunk_s, chunk_xy0, x, y);
-                int W = P.W, H = P.H;
-                asm volatile("" : "+s"(W), "+s"(H));
-                bool ok = x < W && y < H;
-                if (ok) {
-                    if (P.rays) {
-                        float4 r = P.rays[item];
-                        d = v3(r.x, r.y, r.z);
-                        st = __float_as_uint(r.w);
-                        float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
-                        asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
-                        o = v3(o0, o1, o2);
-                    } else {
-                        camera_ray(P, x, y, chunk_s, st, o, d);
-                    }
-                }
-                if (!ok) {
-                    float* out = P.out + (size_t)item * 3;
-                    out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
-                    item = -2;  // served, nothing to trace this iteration
-                } else {
-                    beta = v3(1, 1, 1);
-                    bounce = 0;
-                    qtype = Q_EXT;
-                    tmax = kTMax;
-                }
-            }
-            q_next += take;
-            idle = __ballot(item == -1);
-        }
-        if (item == -2) item = -1;
-        if (__ballot(item >= 0) == 0) {
-            if (exhausted && q_next == q_end) break;
-            continue;
-        }
-        if (item < 0) continue;
-        if (PHASE && (qtype == Q_SHADOW) != do_shadow) continue;
-
-        // ------------------------------------------------------- one query
-        int hid = -1;
-        float ht = 0.0f;
-        bool hit;
-        if (STATS) {
-            if (!pending) {
-                if (qtype == Q_EXT) cn.ext++; else cn.shadow++;
-            }
-            // wave-level clocks: the first active lane books the interval
-            const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
-            const uint64_t active = __ballot(true);
-            t_b = __builtin_amdgcn_s_memtime();
-            if (leader) {
-                c_refill += t_b - t_a;
-                n_iter++;
-                n_active += (uint64_t)__popcll(active);
-            }
-            t_a = t_b;
-        }
-        if (TRAV == 0) {
-            if (qtype == Q_EXT) hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
-            else hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
-        } else if (TRAV == 1) {
-            hit = traverse_u<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
-        } else if (TRAV == 2) {
-            hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
-        } else if (TRAV == 3 && RESUME) {
-            if (!pending) tstate_init(tst, stk, tmax);
-            bool done;
-            if (PHASE && do_shadow)
-                done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn,
-                                                                  &tst, P.resume_min, P.fault);
-            else if (PHASE)
-                done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht,
-                                                                  cn, &tst, P.resume_min, P.fault);
-            else
-                done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk,
-                                                                  hid, ht, cn, &tst, P.resume_min, P.fault);
-            pending = !done;
-            if (pending) continue;   // resume next iteration; no shading yet
-            hit = hid >= 0;
-        } else if (TRAV == 3 && PHASE) {
-            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn, nullptr, 0, P.fault);
-            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn, nullptr, 0, P.fault);
-        } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault);
-        } else {
-            park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
-            park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
-            park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
-            asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault);
-            asm volatile("" ::: "memory");
-            float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
-            beta = v3(k0.x, k0.y, k0.z);
-            L = v3(k0.w, k1.x, k1.y);
-            pend = v3(k1.z, k1.w, k2.x);
-            wi = v3(k2.y, k2.z, k2.w);
-        }
-
-        if (P.n_sph > 0 && !(qtype == Q_SHADOW && hit)) {
-            // analytic spheres after the triangles (ids n_tri + k), same rule as the oracle
-            float best = hit ? ht : tmax;
-            for (int k = 0; k < P.n_sph; ++k) {
-                float root;
-                if (sphere_hit(P.sph[k], o, d, kTMin, best, root)) {
-                    best = root;
-                    hid = P.n_tri + k;
-                    hit = true;
-                    if (qtype == Q_SHADOW) break;
-                }
-            }
-            ht = best;
-        }
-        if (STATS) {
-            const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
-            t_b = __builtin_amdgcn_s_memtime();
-            if (leader) c_trav += t_b - t_a;
-            t_a = t_b;
-            // wave-level loop trips = max over the participating lanes; lane-level = sum
-            uint32_t mi = cn.it_inner, ml = cn.it_leaf;
-            for (int off = 32; off > 0; off >>= 1) {
-                mi = max(mi, (uint32_t)__shfl_xor((int)mi, off));
-                ml = max(ml, (uint32_t)__shfl_xor((int)ml, off));
-            }
-            if (leader) { w_inner += mi; w_leaf += ml; }
-            l_inner += cn.it_inner; l_leaf += cn.it_leaf;
-            cn.it_inner = 0; cn.it_leaf = 0;
-        }
-        // ------------------------------------------------- shade the result
-        bool finished = false;
-        if (qtype == Q_EXT) {
-            if (!hit) {
-                finished = true;
-            } else {
-                V3 p = o + d * ht;                                         // ray.at
-                V3 ng;
-                int mid;
-                if (hid < P.n_tri) {
-                    float4 nm = s_nm[hid];
-                    ng = xyz(nm);
-                    mid = __float_as_int(nm.w);
-                } else {                                                   // sphere: (p - c) / r
-                    asm volatile("");   // keep the divisions in this branch (no if-conversion)
-                    float4 sc = P.sph[hid - P.n_tri];
-                    ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
-                    mid = P.sph_mat[hid - P.n_tri];
-                }
-                const float* m = s_mats + 8 * mid;
-                const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;   // shapes.py:101-102
-                const V3 n = flip ? neg(ng) : ng;
-                if (m[5] == 2.0f || m[5] == 3.0f) {
-                    // specular BSDFs (build-added, config 3; bsdf_taichi.py:52-59, :69-86):
-                    // delta distributions, beta *= albedo, no NEE
-                    bool front = dot(d, ng) < 0.0f;
-                    V3 ns = front ? ng : neg(ng);
-                    V3 unit = normalize(d);
-                    V3 out;
-                    bool absorbed = false;
-                    if (m[5] == 2.0f) {
-                        out = reflect3(unit, ns);
-                        if (m[7] > 0.0f) out = out + random_in_unit_sphere(st) * m[7];
-                        absorbed = !(dot(out, ns) > 0.0f);
-                    } else {
-                        float ratio = front ? 1.0f / m[6] : m[6];
-                        float ct = -dot(unit, ns);
-                        ct = ct > 1.0f ? 1.0f : ct;
-                        float stn = sqrtf(1.0f - ct * ct);
-                        bool cannot = ratio * stn > 1.0f;
-                        if (cannot || schlick(ct, ratio) > rng_next(st)) out = reflect3(unit, ns);
-                        else out = refract3(unit, ns, ratio);
-                    }
-                    if (absorbed) {
-                        finished = true;
-                    } else {
-                        beta = beta * v3(m[0], m[1], m[2]);
-                        o = p;
-                        d = normalize(out);
-                        ++bounce;
-                        if (bounce >= P.depth) finished = true;
-                    }
-                } else if (m[3] != 0.0f) {                                 // tracing.py:129-139
-                    float d1 = dot(neg(d), n);
-                    if (d1 > 0.0f) {
-                        V3 lc = v3(P.dl_r, P.dl_g, P.dl_b);
-                        L = bounce == 0 ? L + lc * beta : L + (lc * beta) * d1;
-                    }
-                    finished = true;
-                } else {
-                    // BSDFLambertian.scatter + frame (bsdf.py:29-34, shapes.py:105-108).
-                    // Triangles read rotate_z_to's rows precomputed on the host with the
-                    // same f32 arithmetic (per face and side); spheres build them here.
-                    float u0 = rng_next(st);
-                    float u1 = rng_next(st);
-                    V3 l = cosine_hemisphere(u0, u1);
-                    if (hid < P.n_tri) {
-                        const float4* fr = s_fr + ((size_t)hid * 2 + (flip ? 1 : 0)) * 3;
-                        float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
-                        wi = normalize(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
-                    } else {
-                        wi = to_world(n, l);
-                    }
-                    float pdf = fabsf(dot(n, wi)) * kInvPi;
-                    V3 att = v3(m[0], m[1], m[2]);
-                    float cw = dot(n, wi);
-                    float dz = cw > 0.0f ? cw : 0.0f;
-                    // tracing.py:146-148: if any component of att*dz/pdf*InvPi is NaN the
-                    // reference recomputes it with pdf = 1e-4.  (a / pdf) * InvPi is NaN
-                    // exactly when a / pdf is, so the condition is decided before dividing.
-                    V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                    if (div_is_nan(ad.x, pdf) || div_is_nan(ad.y, pdf) || div_is_nan(ad.z, pdf)) pdf = 1e-4f;
-                    V3 nb = v3(ad.x / pdf * kInvPi, ad.y / pdf * kInvPi, ad.z / pdf * kInvPi);
-                    beta = beta * nb;
-                    // sample_direct_lighting (tracing.py:92-108)
-                    int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
-                    int lo = s_loff[li];
-                    int f = rng_int(st, 0, s_loff[li + 1] - lo - 1);
-                    float su = sqrtf(rng_next(st));
-                    float sv = rng_next(st);
-                    float a = su * (1.0f - sv);
-                    float b = su * sv;
-                    const float4* lv = s_lv + (size_t)(lo + f) * 4;
-                    float4 L0 = lv[0], L1 = lv[1], L2 = lv[2], LN = lv[3];
-                    float c = 1.0f - a - b;
-                    V3 p2 = (xyz(L0) * a + xyz(L1) * b) + xyz(L2) * c;
-                    V3 n2 = xyz(LN);
-                    V3 w = normalize(p2 - p);
-                    float t_at = (p2.x - p.x) / w.x;
-                    // w2 = normalize(p - p2) is -w bit for bit (round-to-nearest is sign
-                    // symmetric) up to the sign of zero components, so dot(n2, w2) =
-                    // -dot(n2, w) except for the sign of a zero result, which the
-                    // strict "> 0" test and the uses below cannot see.
-                    float dot1 = dot(n, w), dot2 = -dot(n2, w);
-                    o = p;
-                    if (dot1 > 0.0f && dot2 > 0.0f) {
-                        const float* em = s_mats + 8 * __float_as_int(LN.w);
-                        V3 dd = p - p2;
-                        float sl = dot(dd, dd);
-                        V3 rad = v3(em[0] * dot1 * dot2 / sl, em[1] * dot1 * dot2 / sl, em[2] * dot1 * dot2 / sl);
-                        pend = beta * rad;
-                        d = w;
-                        tmax = t_at;
-                        qtype = Q_SHADOW;
-                    } else {
-                        // no NEE term possible: go straight to the next bounce
-                        ++bounce;
-                        if (bounce >= P.depth) finished = true;
-                        d = wi;
-                        tmax = kTMax;
-                    }
-                }
-            }
-        } else {
-            if (!hit) L = L + pend;
-            ++bounce;
-            if (bounce >= P.depth) finished = true;
-            d = wi;           // o is still the hit point p
-            tmax = kTMax;
-            qtype = Q_EXT;
-        }
-        if (finished) {
-            float* out = P.out + (size_t)item * 3;
-            out[0] = L.x; out[1] = L.y; out[2] = L.z;
-            item = -1;
-        }
-        if (STATS) {
-            const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
-            if (leader) c_shade += __builtin_amdgcn_s_memtime() - t_a;
-        }
-    }
-    if (STATS) {
-        uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_down(a, off); b += __shfl_down(b, off);
-            c += __shfl_down(c, off); e += __shfl_down(e, off);
-        }
-        uint64_t wv[7] = {c_refill, c_trav, c_shade, n_iter, n_active, w_inner, w_leaf};
-        for (int k = 0; k < 7; ++k)
-            for (int off = 32; off > 0; off >>= 1) wv[k] += __shfl_down(wv[k], off);
-        if (lane == 0) {
-            atomicAdd(P.stats + 0, (unsigned long long)a);
-            atomicAdd(P.stats + 1, (unsigned long long)b);
-            atomicAdd(P.stats + 2, (unsigned long long)c);
-            atomicAdd(P.stats + 3, (unsigned long long)e);
-            for (int k = 0; k < 7; ++k) atomicAdd(P.stats + 4 + k, (unsigned long long)wv[k]);
-        }
-        {
-            uint32_t m = cn.max_sp;
-            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_down((int)m, off));
-            if (lane == 0) atomicMax(P.stats + 13, (unsigned long long)m);
-        }
-        {
-            uint64_t a2 = l_inner, b2 = l_leaf;
-            for (int off = 32; off > 0; off >>= 1) { a2 += __shfl_down(a2, off); b2 += __shfl_down(b2, off); }
-            if (lane == 0) {
-                atomicAdd(P.stats + 11, (unsigned long long)a2);
-                atomicAdd(P.stats + 12, (unsigned long long)b2);
-            }
-        }
-    }
 }
 
 // World.hit_all for a batch of rays (intersection_taichi.py:238-291): closest (or any)
@@ -1241,67 +101,6 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
 
 }  // namespace
 
-// variant table: (traversal | 8 phase-aligned, LDS scene, min waves per SIMD); see prt_kernels.h
-#define PRT_VARIANTS(X)                                   \
-    X(kVarSplit, 0, false, 1)                             \
-    X(kVarUnified, 1, false, 1)                           \
-    X(kVarUnifiedLds, 1, true, 1)                         \
-    X(kVarWW, 2, false, 1)                                \
-    X(kVarWWLds, 2, true, 1)                              \
-    X(kVarWWLds5, 2, true, 5)                             \
-    X(kVarWWLds6, 2, true, 6)                             \
-    X(kVarWW5, 2, false, 5)                               \
-    X(kVarWW4, 3, false, 1)                               \
-    X(kVarWW4Lds, 3, true, 1)                             \
-    X(kVarWW4Lds6, 3, true, 6)                            \
-    X(kVarWW4ParkLds6, 4, true, 6)                        \
-    X(kVarWW4ParkLds7, 4, true, 7)                        \
-    X(kVarWW4Park5, 4, false, 5)                        \
-    X(kVarWW4PhLds6, 11, true, 6)                        \
-    X(kVarWW4PhLds, 11, true, 1)                         \
-    X(kVarWW4Ph, 11, false, 1)                           \
-    X(kVarWW4Ph5, 11, false, 5)                          \
-    X(kVarWW4Sp, 35, false, 1)                           \
-    X(kVarWW4Sp4, 35, false, 4)                          \
-    X(kVarWW4Sp5, 35, false, 5)                          \
-    X(kVarWW4QSp, 99, false, 1)                          \
-    X(kVarWW4QSp5, 99, false, 5)                         \
-    X(kVarWW4QPhSp, 107, false, 1)                       \
-    X(kVarWW4QSp6, 99, false, 6)                         \
-    X(kVarWW4PhRLds6, 139, true, 6)                      \
-    X(kVarWW4RLds6, 131, true, 6)                        \
-    X(kVarWW4QRSp5, 227, false, 5)                       \
-    X(kVarWW4PhLds7, 11, true, 7)                        \
-    X(kVarWW4PhLds5, 11, true, 5)
-
-// spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
-template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
-static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStream_t stream) {
-    constexpr bool spill = (VAR & 32) != 0;
-    if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
-        trace_kernel<STACK, STATS, VAR, LDS, WPE><<<grid, kBlock, smem, stream>>>(P);
-        return hipGetLastError();
-    } else {
-        return hipErrorInvalidValue;
-    }
-}
-
-template <int STACK, bool STATS>
-static hipError_t launch_var(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream) {
-    switch (var) {
-#define X(id, trav, lds, wpe) \
-        case id: return launch_one<STACK, STATS, trav, lds, wpe>(P, grid, smem, stream);
-        PRT_VARIANTS(X)
-#undef X
-        default: return hipErrorInvalidValue;
-    }
-}
-
-template <int STACK>
-static hipError_t launch_stack(const TraceParams& P, int var, int grid, bool stats, size_t smem, hipStream_t stream) {
-    return stats ? launch_var<STACK, true>(P, var, grid, smem, stream) : launch_var<STACK, false>(P, var, grid, smem, stream);
-}
-
 bool variant_uses_lds(int var);
 
 // entries needed: one per level (<= depth) plus the while-while sentinel
@@ -1331,11 +130,11 @@ size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream) {
     size_t smem = trace_smem_bytes(stack, var, P);
     switch (stack) {
-        case 4: return launch_stack<4>(P, var, grid, stats, smem, stream);
-        case 10: return launch_stack<10>(P, var, grid, stats, smem, stream);
-        case 16: return launch_stack<16>(P, var, grid, stats, smem, stream);
-        case 32: return launch_stack<32>(P, var, grid, stats, smem, stream);
-        default: return launch_stack<64>(P, var, grid, stats, smem, stream);
+        case 4: return stats ? launch_trace_4_1(P, var, grid, smem, stream) : launch_trace_4_0(P, var, grid, smem, stream);
+        case 10: return stats ? launch_trace_10_1(P, var, grid, smem, stream) : launch_trace_10_0(P, var, grid, smem, stream);
+        case 16: return stats ? launch_trace_16_1(P, var, grid, smem, stream) : launch_trace_16_0(P, var, grid, smem, stream);
+        case 32: return stats ? launch_trace_32_1(P, var, grid, smem, stream) : launch_trace_32_0(P, var, grid, smem, stream);
+        default: return stats ? launch_trace_64_1(P, var, grid, smem, stream) : launch_trace_64_0(P, var, grid, smem, stream);
     }
 }
 
@@ -1366,26 +165,6 @@ hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, b
     return hipGetLastError();
 }
 
-template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
-static void occ_one(int* n, size_t smem) {
-    constexpr bool spill = (VAR & 32) != 0;
-    if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(n, trace_kernel<STACK, STATS, VAR, LDS, WPE>, kBlock, smem);
-}
-
-template <int STACK, bool STATS>
-static int occ_var(int var, size_t smem) {
-    int n = 0;
-    switch (var) {
-#define X(id, trav, lds, wpe) \
-        case id: occ_one<STACK, STATS, trav, lds, wpe>(&n, smem); break;
-        PRT_VARIANTS(X)
-#undef X
-        default: break;
-    }
-    return n;
-}
-
 bool variant_uses_bvh4(int var) {
     switch (var) {
 #define X(id, trav, lds, wpe) case id: return (trav & 7) >= 3;
@@ -1413,6 +192,15 @@ bool variant_spills(int var) {
     }
 }
 
+bool variant_drains(int var) {
+    switch (var) {
+#define X(id, trav, lds, wpe) case id: return (trav & 256) != 0;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
 bool variant_uses_lds(int var) {
     switch (var) {
 #define X(id, trav, lds, wpe) case id: return lds;
@@ -1424,11 +212,11 @@ bool variant_uses_lds(int var) {
 
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem) {
     switch (stack) {
-        case 4: return stats ? occ_var<4, true>(var, smem) : occ_var<4, false>(var, smem);
-        case 10: return stats ? occ_var<10, true>(var, smem) : occ_var<10, false>(var, smem);
-        case 16: return stats ? occ_var<16, true>(var, smem) : occ_var<16, false>(var, smem);
-        case 32: return stats ? occ_var<32, true>(var, smem) : occ_var<32, false>(var, smem);
-        default: return stats ? occ_var<64, true>(var, smem) : occ_var<64, false>(var, smem);
+        case 4: return stats ? trace_occ_4_1(var, smem) : trace_occ_4_0(var, smem);
+        case 10: return stats ? trace_occ_10_1(var, smem) : trace_occ_10_0(var, smem);
+        case 16: return stats ? trace_occ_16_1(var, smem) : trace_occ_16_0(var, smem);
+        case 32: return stats ? trace_occ_32_1(var, smem) : trace_occ_32_0(var, smem);
+        default: return stats ? trace_occ_64_1(var, smem) : trace_occ_64_0(var, smem);
     }
 }
 

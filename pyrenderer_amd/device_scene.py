@@ -12,10 +12,45 @@ def tile_grid(W, H, tile):
     return tx, ty
 
 
-def interleaved_tiles(W, H, tile, rank=0, world=1):
-    """Tile ids owned by `rank` of `world`: id % world == rank."""
+def latin_stride(world):
+    """Row shift s of the 'latin' tile assignment: the integer nearest 0.38 * world
+    (a golden-ratio-like step) that is coprime with world, so consecutive tile rows are
+    shifted by s and, when world divides the tile columns, every rank owns exactly one
+    tile in each run of `world` columns of every row."""
+    import math
+    s = max(1, int(round(0.38 * world)))
+    while math.gcd(s, world) != 1:
+        s += 1
+    return s
+
+
+def tile_owner(W, H, tile, world, scheme="latin"):
+    """Owner rank of every tile id (ty * tiles_x + tx) — SURVEY.md §8e's interleaving.
+
+    'mod'  : id % world.  On a frame whose tile columns are a multiple of world this
+             hands each rank whole tile COLUMNS (8 x 8 tiles at world 8), so ranks see
+             different parts of the scene and the slowest one sets the step time.
+    'latin': (tx + s * ty) % world with s = latin_stride(world): each rank owns tiles
+             spread over every row and column of the frame (a Latin square when world
+             divides the tile columns), which evens out the per-rank path cost."""
     tx, ty = tile_grid(W, H, tile)
-    return np.arange(rank, tx * ty, world, dtype=np.int32)
+    ids = np.arange(tx * ty, dtype=np.int64)
+    if world <= 1:
+        return np.zeros(tx * ty, np.int32)
+    if scheme == "mod":
+        return (ids % world).astype(np.int32)
+    if scheme == "latin":
+        return ((ids % tx + latin_stride(world) * (ids // tx)) % world).astype(np.int32)
+    raise ValueError(f"unknown tile scheme {scheme!r}")
+
+
+def interleaved_tiles(W, H, tile, rank=0, world=1, scheme="latin"):
+    """Tile ids owned by `rank` of `world`, ascending (see tile_owner)."""
+    return np.nonzero(tile_owner(W, H, tile, world, scheme) == rank)[0].astype(np.int32)
+
+
+def max_tiles_per_rank(W, H, tile, world, scheme="latin"):
+    return int(np.bincount(tile_owner(W, H, tile, world, scheme), minlength=max(world, 1)).max())
 
 
 def unpack_tiles(slots, W, H, tw, th, tile_ids, frame=None):

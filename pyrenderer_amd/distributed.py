@@ -1,7 +1,8 @@
 """One process per GPU: interleaved tile sharding + RCCL gather.
 
-Every rank renders the 64x64 tiles with id % world == rank (load balance over
-the light-heavy and escape-heavy parts of the frame) into a device buffer of
+Every rank renders the 64x64 tiles that device_scene.tile_owner assigns it (the
+'latin' interleaving: tiles spread over every row and column of the frame, so
+light-heavy and escape-heavy regions are shared evenly) into a device buffer of
 per-tile radiance sums; the buffers are gathered to rank 0 with
 torch.distributed (backend "nccl" = RCCL over xGMI on MI355X; "gloo" on CPU
 for tests) and rank 0 scatters the tiles into the (W, H, 3) frame.  Random
@@ -12,18 +13,19 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .device_scene import interleaved_tiles, tile_grid, unpack_tiles
+from .device_scene import interleaved_tiles, max_tiles_per_rank, tile_grid, unpack_tiles
 
 
 class TileShard:
     """This rank's tiles and the padded gather buffers (allocated once)."""
 
-    def __init__(self, W, H, tile, rank, world, device):
+    def __init__(self, W, H, tile, rank, world, device, scheme="latin"):
         self.W, self.H, self.tile, self.rank, self.world = W, H, tile, rank, world
+        self.scheme = scheme
         tx, ty = tile_grid(W, H, tile)
         self.n_tiles = tx * ty
-        self.tiles = interleaved_tiles(W, H, tile, rank, world)
-        self.max_tiles = (self.n_tiles + world - 1) // world
+        self.tiles = interleaved_tiles(W, H, tile, rank, world, scheme)
+        self.max_tiles = max_tiles_per_rank(W, H, tile, world, scheme)
         self.slot_elems = tile * tile * 3
         self.buf = torch.zeros(self.max_tiles * self.slot_elems, dtype=torch.float32, device=device)
         self.gather_list = ([torch.empty_like(self.buf) for _ in range(world)]
@@ -39,7 +41,7 @@ class TileShard:
         frame = np.zeros((self.W, self.H, 3), np.float32)
         bufs = self.gather_list if self.world > 1 else [self.buf]
         for r, b in enumerate(bufs):
-            ids = interleaved_tiles(self.W, self.H, self.tile, r, self.world)
+            ids = interleaved_tiles(self.W, self.H, self.tile, r, self.world, self.scheme)
             n = len(ids) * self.slot_elems
             unpack_tiles(b[:n].cpu().numpy().reshape(-1, 3), self.W, self.H, self.tile, self.tile, ids, frame)
         return frame

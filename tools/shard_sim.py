@@ -1,0 +1,86 @@
+"""Predict multi-GPU tile balance on ONE GPU: render, one rank at a time, exactly the
+tiles rank r of N would own (device_scene.tile_owner) and time it.  The slowest
+rank's time bounds the N-GPU step (plus the gather); T1 / (N * max_r T_r) is the
+balance-limited strong-scaling efficiency.
+
+    python tools/shard_sim.py [--config 2] [--tiles 64,32] [--schemes mod,latin] [--worlds 2,4,8]
+
+Prints one JSON line per (tile, scheme, world).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--tiles", default="64,32")
+    ap.add_argument("--schemes", default="mod,latin")
+    ap.add_argument("--worlds", default="2,4,8")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--streams", type=int, default=1, help="frames in flight, as bench.py --streams")
+    ap.add_argument("--variant", type=int, default=0)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import bench
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles, max_tiles_per_rank
+    from pyrenderer_amd.flatten import flatten_scene
+
+    cfg = bench.CONFIGS[a.config]
+    scene, camera = bench.load_scene(cfg["scene"])
+    flat = flatten_scene(scene)
+    cam = camera.convert_to_taichi_camera().packed()
+    ds = DeviceScene(flat, 0)
+    W = H = cfg["res"]
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(a.streams - 1)]
+
+    def time_tiles(tile, ids):
+        bufs = [torch.empty(max(len(ids), 1) * tile * tile * 3, dtype=torch.float32, device=dev) for _ in streams]
+        for b, st in zip(bufs, streams):
+            ds.render_tiles_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], b.data_ptr(), st.cuda_stream,
+                                   flags=a.variant << 8)
+        torch.cuda.synchronize(dev)
+        ds.kernel_timing()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            k = i % len(streams)
+            ds.render_tiles_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], bufs[k].data_ptr(),
+                                   streams[k].cuda_stream, flags=N.PRT_FLAG_TIME | (a.variant << 8))
+        torch.cuda.synchronize(dev)
+        wall = (time.perf_counter() - t0) * 1e3 / a.steps
+        kms, launches = ds.kernel_timing()
+        return wall, kms / max(launches, 1)
+
+    for tile in [int(t) for t in a.tiles.split(",")]:
+        t1_wall, t1_k = time_tiles(tile, interleaved_tiles(W, H, tile))
+        print(json.dumps({"tile": tile, "world": 1, "streams": a.streams, "variant": a.variant, "wall_ms": round(t1_wall, 4), "kernel_ms": round(t1_k, 4)}),
+              flush=True)
+        for scheme in a.schemes.split(","):
+            for world in [int(w) for w in a.worlds.split(",")]:
+                walls, kerns = [], []
+                for r in range(world):
+                    w, k = time_tiles(tile, interleaved_tiles(W, H, tile, r, world, scheme))
+                    walls.append(w)
+                    kerns.append(k)
+                print(json.dumps({
+                    "tile": tile, "scheme": scheme, "world": world, "streams": a.streams,
+                    "max_tiles": max_tiles_per_rank(W, H, tile, world, scheme),
+                    "wall_ms": [round(x, 4) for x in walls], "kernel_ms": [round(x, 4) for x in kerns],
+                    "kernel_max_over_mean": round(max(kerns) / (sum(kerns) / world), 4),
+                    "eff_wall": round(t1_wall / (world * max(walls)), 4),
+                    "eff_kernel": round(t1_k / (world * max(kerns)), 4)}), flush=True)
+    ds.close()
+
+
+if __name__ == "__main__":
+    main()
