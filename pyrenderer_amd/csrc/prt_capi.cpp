@@ -87,7 +87,7 @@ struct DevBuf {
 // work counter + watchdog flag, the spill area and the host-output sums.
 struct RenderCtx {
     hipStream_t stream = nullptr;
-    DevBuf tiles, buf, rays, work, acc, spill, cont, cont_flag;
+    DevBuf tiles, buf, rays, work, acc, spill;
     std::vector<uint32_t> tile_host;
     uint64_t last_use = 0;
 };
@@ -115,7 +115,6 @@ struct Scene {
     int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
     int need4 = 0;                   // worst-case BVH4 traversal stack entries
     int resume_min = 16;             // resume variants (env PRT_RESUME_MIN)
-    int drain_push = 16;             // drain variants (env PRT_DRAIN_PUSH, 0..64)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
     int64_t n_sph = 0;
     DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
@@ -149,7 +148,7 @@ void destroy_scene(Scene* s) {
         b->release();
     if (!s->ctx.empty()) (void)hipDeviceSynchronize();
     for (auto& c : s->ctx)
-        for (DevBuf* b : {&c->tiles, &c->buf, &c->rays, &c->work, &c->acc, &c->spill, &c->cont, &c->cont_flag})
+        for (DevBuf* b : {&c->tiles, &c->buf, &c->rays, &c->work, &c->acc, &c->spill})
             b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -174,10 +173,7 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
     return PRT_OK;
 }
 
-constexpr size_t prt_cont_bytes() { return 12 * sizeof(unsigned long long); }  // prt_device.h kContWords
-
-// work.p: [0] chunk counter, [1..3] drain hand-off counters (published, claimed, exited
-// waves); [kFaultOffset] traversal watchdog flag (bit 1: lost hand-off)
+// work.p: [0] chunk counter; [kFaultOffset] traversal watchdog flag
 constexpr size_t kFaultOffset = 32;
 
 int read_fault_at(const DevBuf& work) {
@@ -307,7 +303,6 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     {
         P.cam_fast = cam_fast ? 1 : 0;
         P.resume_min = s->resume_min;
-        P.drain_push = s->drain_push;
         P.rays = primary ? (const float4*)cx->rays.p : nullptr;
         const float rd2 = -cam[18];
         for (int i = 0; i < 3; ++i) {
@@ -359,15 +354,6 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         P.spill = (int*)cx->spill.p;
     }
 
-    const bool drain = prt::variant_drains(var);
-    const size_t grid_lanes = (size_t)occ * s->cus * 256;
-    if (drain) {
-        // one continuation slot per lane of the largest grid (a path is published at most once)
-        HIP_TRY(cx->cont.ensure(grid_lanes * prt_cont_bytes()));
-        HIP_TRY(cx->cont_flag.ensure(grid_lanes * sizeof(uint32_t)));
-        P.cont = (unsigned long long*)cx->cont.p;
-        P.cont_flag = (uint32_t*)cx->cont_flag.p;
-    }
     int64_t n_chunks = (spp + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
     int k = s->ev_used / 2;
@@ -386,7 +372,6 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
         HIP_TRY(hipMemsetAsync(cx->work.p, 0, 16, stream));
-        if (drain) HIP_TRY(hipMemsetAsync(cx->cont_flag.p, 0, sizeof(uint32_t) * (size_t)grid * 256, stream));
         if (primary) HIP_TRY(prt::launch_camera(P, (float4*)cx->rays.p, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
         HIP_TRY(prt::launch_trace(P, stack, var, grid, stats, stream));
@@ -555,7 +540,6 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         s->n_node_f4 = (int64_t)bvh.nodes.size() / 4;
         s->n_tri_f4 = (int64_t)bvh.tris.size() / 4;
         if (const char* rm = std::getenv("PRT_RESUME_MIN")) s->resume_min = std::max(1, std::min(64, std::atoi(rm)));
-        if (const char* dp = std::getenv("PRT_DRAIN_PUSH")) s->drain_push = std::max(0, std::min(64, std::atoi(dp)));
         if (const char* sl = std::getenv("PRT_SPILL_LDS")) {
             int v = std::atoi(sl);
             s->spill_lds = v == 4 ? 4 : v == 32 ? 32 : 16;

@@ -753,43 +753,6 @@ __device__ __forceinline__ void camera_ray(const TraceParams& P, int x, int y, u
 
 enum : int { Q_EXT = 0, Q_SHADOW = 1 };
 
-// ------------------------------------------------------------ drain hand-off
-// When the work queue is exhausted, every wave still holds paths that started at
-// about the same time, so all blocks finish together one path latency later and
-// the CUs idle meanwhile (the ~0.3 ms launch tail).  DRAIN variants compact that
-// tail: a wave left with <= P.drain_push active lanes publishes its paths (96 B of
-// state each) to a global continuation buffer and exits; waves with idle lanes pull
-// them.  Blocks then retire progressively (the next frame's launch, on another
-// stream, fills the freed CUs) and the last paths run in a few densely packed waves.
-// Visibility across XCDs (MI355X_MICROARCH.md, inter-workgroup visibility): the
-// payload is stored write-through (agent-scope relaxed atomics = sc1 stores), the
-// storing wave drains with s_waitcnt vmcnt(0), then each lane stores its slot's flag
-// the same way; the consumer polls the flag with sc1 loads and reads the payload with
-// sc1 loads only (no L1-resident copy can be stale).  Results are bit-identical: a
-// path carries its RNG state and work item, so the lane running it does not matter.
-typedef __attribute__((address_space(1))) unsigned long long g_u64;
-typedef __attribute__((address_space(1))) unsigned int g_u32;
-constexpr int kContWords = 12;            // u64 words of one path state
-constexpr uint32_t kDrainSpin = 1u << 22;  // flag polls before a hand-off is declared lost
-
-__device__ __forceinline__ unsigned long long pack2(float a, float b) {
-    return (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
-}
-__device__ __forceinline__ unsigned long long pack2u(uint32_t a, uint32_t b) {
-    return (unsigned long long)a | ((unsigned long long)b << 32);
-}
-__device__ __forceinline__ float lo_f(unsigned long long w) { return __uint_as_float((uint32_t)w); }
-__device__ __forceinline__ float hi_f(unsigned long long w) { return __uint_as_float((uint32_t)(w >> 32)); }
-__device__ __forceinline__ void st_sc1(unsigned long long* p, unsigned long long v) {
-    __hip_atomic_store((g_u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld_sc1(const unsigned long long* p) {
-    return __hip_atomic_load((g_u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
-    return __hip_atomic_load((g_u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel(TraceParams P) {
@@ -800,8 +763,6 @@ void trace_kernel(TraceParams P) {
     constexpr bool SPILL = (VAR & 32) != 0;    // LDS stack of STACK entries + global spill area
     constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
     constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
-    constexpr bool DRAIN = (VAR & 256) != 0;   // compact the launch tail through the continuation buffer
-    static_assert(!(DRAIN && RESUME), "drain hand-off does not carry suspended traversal state");
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
     // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
@@ -854,7 +815,6 @@ void trace_kernel(TraceParams P) {
     // wave-uniform work queue [q_next, q_end)
     uint32_t q_next = 0, q_end = 0;
     bool exhausted = false;
-    bool sticky = false;    // DRAIN: this wave has pulled continuations and never publishes any
 
     // lane state
     TState tst = {0, 0, 0, -1, 0.0f};
@@ -947,116 +907,8 @@ void trace_kernel(TraceParams P) {
             idle = __ballot(item == -1);
         }
         if (item == -2) item = -1;
-        if constexpr (DRAIN) {
-            if (!do_shadow && exhausted && q_next == q_end) {
-                uint32_t* ctr = P.work;   // [1] published (tail), [2] claimed (head), [3] exited waves
-                // pull continuations into idle lanes
-                uint64_t idle2 = __ballot(item == -1);
-                if (idle2) {
-                    uint32_t got = 0, base = 0;
-                    if (lane == (int)__builtin_amdgcn_readfirstlane(lane)) {
-                        uint32_t need = (uint32_t)__popcll(idle2);
-                        while (true) {
-                            uint32_t h = ld_sc1_u32(ctr + 2), t = ld_sc1_u32(ctr + 1);
-                            if (h >= t) break;
-                            uint32_t n = min(need, t - h);
-                            if (atomicCAS(ctr + 2, h, h + n) == h) { got = n; base = h; break; }
-                        }
-                    }
-                    got = __builtin_amdgcn_readfirstlane(got);
-                    base = __builtin_amdgcn_readfirstlane(base);
-                    if (got) {
-                        sticky = true;
-                        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle2 >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)idle2, 0u));
-                        if (((idle2 >> lane) & 1ull) && rank < got) {
-                            uint32_t slot = base + rank;
-                            uint32_t spins = 0;
-                            while (ld_sc1_u32(P.cont_flag + slot) == 0u && ++spins < kDrainSpin)
-                                __builtin_amdgcn_s_sleep(1);
-                            if (spins >= kDrainSpin) {
-                                atomicOr(P.fault, 2);   // lost hand-off: results invalid
-                            } else {
-                                const unsigned long long* c = P.cont + (size_t)slot * kContWords;
-                                unsigned long long w[kContWords];
-#pragma unroll
-                                for (int k = 0; k < kContWords; ++k) w[k] = ld_sc1(c + k);
-                                item = (int)(uint32_t)w[0];
-                                bounce = (int)(uint32_t)(w[0] >> 32);
-                                st = (uint32_t)w[1];
-                                qtype = (int)(uint32_t)(w[1] >> 32);
-                                o = v3(lo_f(w[2]), hi_f(w[2]), lo_f(w[3]));
-                                d = v3(hi_f(w[3]), lo_f(w[4]), hi_f(w[4]));
-                                wi = v3(lo_f(w[5]), hi_f(w[5]), lo_f(w[6]));
-                                beta = v3(hi_f(w[6]), lo_f(w[7]), hi_f(w[7]));
-                                L = v3(lo_f(w[8]), hi_f(w[8]), lo_f(w[9]));
-                                pend = v3(hi_f(w[9]), lo_f(w[10]), hi_f(w[10]));
-                                tmax = lo_f(w[11]);
-                            }
-                        }
-                    }
-                }
-                // publish this wave's paths when few remain
-                if (!sticky) {
-                    uint64_t act = __ballot(item >= 0);
-                    if (act != 0 && __popcll(act) <= P.drain_push) {
-                        uint32_t base = 0;
-                        if (lane == (int)__builtin_amdgcn_readfirstlane(lane)) base = atomicAdd(ctr + 1, (uint32_t)__popcll(act));
-                        base = __builtin_amdgcn_readfirstlane(base);
-                        uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                        uint32_t slot = base + rank;
-                        if (item >= 0) {
-                            unsigned long long* c = P.cont + (size_t)slot * kContWords;
-                            st_sc1(c + 0, pack2u((uint32_t)item, (uint32_t)bounce));
-                            st_sc1(c + 1, pack2u(st, (uint32_t)qtype));
-                            st_sc1(c + 2, pack2(o.x, o.y));
-                            st_sc1(c + 3, pack2(o.z, d.x));
-                            st_sc1(c + 4, pack2(d.y, d.z));
-                            st_sc1(c + 5, pack2(wi.x, wi.y));
-                            st_sc1(c + 6, pack2(wi.z, beta.x));
-                            st_sc1(c + 7, pack2(beta.y, beta.z));
-                            st_sc1(c + 8, pack2(L.x, L.y));
-                            st_sc1(c + 9, pack2(L.z, pend.x));
-                            st_sc1(c + 10, pack2(pend.y, pend.z));
-                            st_sc1(c + 11, pack2(tmax, 0.0f));
-                        }
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        if (item >= 0) {
-                            __hip_atomic_store((g_u32*)(P.cont_flag + slot), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            item = -1;
-                        }
-                    }
-                }
-            }
-        }
         if (__ballot(item >= 0) == 0) {
-            if (exhausted && q_next == q_end) {
-                if constexpr (!DRAIN) {
-                    break;
-                } else {
-                    // exit protocol: leave unless continuations are waiting; the last wave to
-                    // leave re-checks, so no published path is ever stranded
-                    uint32_t* ctr = P.work;
-                    uint32_t v = 0;
-                    if (lane == (int)__builtin_amdgcn_readfirstlane(lane)) {
-                        if (ld_sc1_u32(ctr + 2) < ld_sc1_u32(ctr + 1)) {
-                            v = 1;   // pull next iteration
-                        } else {
-                            uint32_t e = atomicAdd(ctr + 3, 1u);
-                            if (e + 1 == gridDim.x * (kBlock / 64)) {
-                                if (ld_sc1_u32(ctr + 2) < ld_sc1_u32(ctr + 1)) {
-                                    atomicSub(ctr + 3, 1u);
-                                    v = 1;
-                                }
-                            }
-                        }
-                    }
-                    v = __builtin_amdgcn_readfirstlane(v);
-                    if (v == 0) break;
-                    continue;
-                }
-            }
+            if (exhausted && q_next == q_end) break;
             continue;
         }
         if (item < 0) continue;
@@ -1357,9 +1209,7 @@ void trace_kernel(TraceParams P) {
     X(kVarWW4RLds6, 131, true, 6)                        \
     X(kVarWW4QRSp5, 227, false, 5)                       \
     X(kVarWW4PhLds7, 11, true, 7)                        \
-    X(kVarWW4PhLds5, 11, true, 5)                        \
-    X(kVarWW4PhLds6D, 267, true, 6)                      \
-    X(kVarWW4QSp5D, 355, false, 5)
+    X(kVarWW4PhLds5, 11, true, 5)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>

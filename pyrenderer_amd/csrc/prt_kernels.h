@@ -23,9 +23,6 @@ struct TraceParams {
     int cam_fast;
     int* fault;               // watchdog flag (non-zero: a traversal exceeded kGuardTrips)
     int resume_min;           // resume variants: leave the traversal loop below this many active lanes
-    int drain_push;           // drain variants: a wave with <= this many active lanes publishes them and exits
-    unsigned long long* cont; // drain variants: continuation buffer, 12 u64 per path, one slot per grid lane
-    uint32_t* cont_flag;      // ... per-slot publish flags (zeroed before the launch)
     int* spill;               // spill variants: per-lane stack entries beyond the LDS part (stride = grid threads)
     const float4* rays;       // primary rays of this launch from camera_kernel, or null (generated in the refill)
     float cam_o[3], cam_k[3];
@@ -80,14 +77,11 @@ constexpr int kVarWW4RLds6 = 27;    // resume, mixed schedule, LDS scene, >= 6 w
 constexpr int kVarWW4QRSp5 = 28;    // resume, quantised nodes, spill stack, >= 5 waves
 constexpr int kVarWW4PhLds7 = 29;   // phase-aligned, LDS scene, >= 7 waves per SIMD
 constexpr int kVarWW4PhLds5 = 30;   // ... >= 5 waves per SIMD
-constexpr int kVarWW4PhLds6D = 31;  // kVarWW4PhLds6 + drain hand-off (compacted launch tail)
-constexpr int kVarWW4QSp5D = 32;    // kVarWW4QSp5 + drain hand-off
-constexpr int kVarLast = 32;
+constexpr int kVarLast = 30;
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
 bool variant_quantized(int var);
 bool variant_uses_bvh4(int var);
-bool variant_drains(int var);
 
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);

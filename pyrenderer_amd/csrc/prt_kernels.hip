@@ -192,15 +192,6 @@ bool variant_spills(int var) {
     }
 }
 
-bool variant_drains(int var) {
-    switch (var) {
-#define X(id, trav, lds, wpe) case id: return (trav & 256) != 0;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
-
 bool variant_uses_lds(int var) {
     switch (var) {
 #define X(id, trav, lds, wpe) case id: return lds;

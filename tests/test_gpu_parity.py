@@ -195,43 +195,6 @@ def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
         assert np.array_equal(g, o), v
 
 
-@pytest.mark.parametrize("push", ["0", "16", "64"])
-def test_drain_handoff_matches_oracle(cornell, oracle_scene, monkeypatch, push):
-    """Drain variants: waves left with <= PRT_DRAIN_PUSH paths publish them to the
-    continuation buffer and exit, other waves pull them.  64: every wave publishes
-    as soon as the queue is empty (maximal hand-off traffic); 0: only the exit
-    protocol.  96x96 x 8 spp = 73,728 samples is well under the ~393 k lanes of the
-    grid, so the queue empties at once and the whole frame runs through the drain."""
-    from pyrenderer_amd import _native as N
-    from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
-    monkeypatch.setenv("PRT_DRAIN_PUSH", push)
-    ds = DeviceScene(cornell[2], 0)
-    cam = cornell[1].convert_to_taichi_camera().packed()
-    for W, spp, tile in ((96, 8, 32), (256, 16, 64)):
-        ids = interleaved_tiles(W, W, tile)
-        o = oracle_scene.render_tiles(cam, W, W, tile, tile, ids, spp, 8, seed=5)
-        g, _ = ds.render_tiles(cam, W, W, tile, tile, ids, spp, 8, 5, N.VAR_WW4_PH_LDS6_DRAIN << 8)
-        assert np.array_equal(g, o), (push, W)
-
-
-def test_drain_handoff_global_scene_matches_oracle(cornell, monkeypatch):
-    """The drain hand-off of the global-memory kernel (quantised BVH4 + spill stack)."""
-    from pyrenderer_amd import _native as N
-    from pyrenderer_amd.device_scene import DeviceScene
-    monkeypatch.setenv("PRT_DRAIN_PUSH", "32")
-    flat = _soup_scene(cornell, 3000, 9)
-    ds = DeviceScene(flat, 0)
-    osc = O.OracleScene.from_flat(flat)
-    cam = cornell[1].convert_to_taichi_camera().packed()
-    o = osc.render(cam, 48, 48, 2, 6, seed=2)
-    from pyrenderer_amd.device_scene import interleaved_tiles, unpack_tiles
-    ids = interleaved_tiles(48, 48, 64)
-    for v in (N.VAR_WW4_Q_SP5, N.VAR_WW4_Q_SP5_DRAIN):
-        sums, _ = ds.render_tiles(cam, 48, 48, 64, 64, ids, 2, 6, 2, v << 8)
-        g = unpack_tiles(sums, 48, 48, 64, 64, ids)
-        assert np.array_equal(g, o), v
-
-
 def test_frames_in_flight_on_two_streams(gpu_scene, oracle_scene, cornell):
     """Two renders enqueued on two HIP streams (one render context each) overlap on the
     device and both return the oracle's frame (bench.py --streams 2)."""
@@ -246,7 +209,7 @@ def test_frames_in_flight_on_two_streams(gpu_scene, oracle_scene, cornell):
     streams = [torch.cuda.Stream(dev) for _ in range(2)]
     outs = [torch.empty(len(ids) * tile * tile * 3, dtype=torch.float32, device=dev) for _ in range(4)]
     for k in range(4):
-        v = (N.VAR_WW4_PH_LDS6_DRAIN if k % 2 else 0) << 8
+        v = (N.VAR_WW4_PH_LDS6 if k % 2 else 0) << 8
         gpu_scene.render_tiles_device(cam, W, W, tile, tile, ids, spp, 8, outs[k].data_ptr(),
                                       streams[k % 2].cuda_stream, seed=7, flags=v)
     torch.cuda.synchronize(dev)
