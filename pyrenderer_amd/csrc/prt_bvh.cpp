@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "prt_internal.h"
@@ -43,12 +44,15 @@ struct TNode {
     int32_t count = 0;               // > 0 for leaves
 };
 
-constexpr int kBins = 16;
+constexpr int kMaxBins = 64;
 
 struct Builder {
     const float* tv;
     int64_t n;
     int max_leaf;
+    int bins = 32;             // SAH bins per axis (env PRT_SAH_BINS, 2..64)
+    double ct = 0.5;           // SAH cost of a node step relative to one triangle test (env PRT_SAH_CT)
+    int leaf_min = 2;          // ranges of <= leaf_min triangles always become leaves (env PRT_LEAF_MIN)
     std::vector<Box> tb;
     std::vector<float> cen;    // n*3
     std::vector<int32_t> idx;  // permutation
@@ -66,7 +70,7 @@ struct Builder {
         }
         nodes[me].box = b;
         max_depth = std::max(max_depth, depth);
-        if (count <= max_leaf && (count <= 2 || depth > 32)) return make_leaf(me, first, count);
+        if (count <= max_leaf && (count <= leaf_min || depth > 32)) return make_leaf(me, first, count);
         if (depth >= 32) {
             // depth guard (bounds the traversal stack): object median on the widest centroid axis
             int ax = 0;
@@ -87,8 +91,9 @@ struct Builder {
         for (int ax = 0; ax < 3; ++ax) {
             float ext = cb.hi[ax] - cb.lo[ax];
             if (!(ext > 0.0f)) continue;
-            Box bins[kBins];
-            int64_t cnt[kBins] = {0};
+            const int kBins = bins;
+            Box bins[kMaxBins];
+            int64_t cnt[kMaxBins] = {0};
             double scale = kBins / (double)ext;
             for (int64_t i = first; i < first + count; ++i) {
                 int k = (int)(((double)cen[3 * (size_t)idx[i] + ax] - cb.lo[ax]) * scale);
@@ -96,8 +101,8 @@ struct Builder {
                 cnt[k]++;
                 bins[k].grow(tb[idx[i]]);
             }
-            double ra[kBins];
-            int64_t rc[kBins];
+            double ra[kMaxBins];
+            int64_t rc[kMaxBins];
             Box acc;
             int64_t c = 0;
             for (int k = kBins - 1; k > 0; --k) {
@@ -115,13 +120,14 @@ struct Builder {
         }
         double parent_area = b.area();
         double leaf_cost = (double)count;
-        double split_cost = parent_area > 0.0 ? 0.5 + best_cost / parent_area : DBL_MAX;
+        double split_cost = parent_area > 0.0 ? ct + best_cost / parent_area : DBL_MAX;
         if (count <= max_leaf && !(split_cost < leaf_cost)) return make_leaf(me, first, count);
         int64_t mid;
         if (best_axis < 0) {
             mid = first + count / 2;  // all centroids coincide: split the range
         } else {
             float ext = cb.hi[best_axis] - cb.lo[best_axis];
+            const int kBins = bins;
             double scale = kBins / (double)ext;
             auto it = std::partition(idx.begin() + first, idx.begin() + first + count, [&](int32_t t) {
                 int k = (int)(((double)cen[3 * (size_t)t + best_axis] - cb.lo[best_axis]) * scale);
@@ -155,6 +161,9 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     if (n_tri < 0 || n_tri >= ((int64_t)1 << 27)) { *err = "triangle count out of range (< 2^27)"; return false; }
     Builder B;
     B.tv = tri_v; B.n = n_tri; B.max_leaf = max_leaf;
+    if (const char* e = std::getenv("PRT_SAH_BINS")) B.bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
+    if (const char* e = std::getenv("PRT_SAH_CT")) B.ct = std::max(0.0, std::atof(e));
+    if (const char* e = std::getenv("PRT_LEAF_MIN")) B.leaf_min = std::max(1, std::min(max_leaf, std::atoi(e)));
     B.tb.resize((size_t)n_tri);
     B.cen.resize((size_t)n_tri * 3);
     B.idx.resize((size_t)n_tri);
