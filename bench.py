@@ -75,7 +75,9 @@ def parse():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--tile", type=int, default=64)
-    ap.add_argument("--streams", type=int, default=2, help="frames in flight (1 = strictly serial frames)")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="frames in flight (1 = strictly serial frames; 0 = auto: 2, or 3 when a rank renders "
+                         "< 8 M samples per frame, where the launch tail is a larger share)")
     ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
@@ -164,7 +166,12 @@ def main():
     t_build = time.perf_counter() - t_build
     W = H = args.res
     T = args.tile
-    n_streams = max(1, args.streams)
+    n_streams = args.streams
+    if n_streams <= 0:
+        # measured (profiles/r01/shard_sim_*): 2 frames in flight are best for a whole C2 frame
+        # on one GPU, 3 for the 1/8 frame of an 8-rank run (0.741 vs 0.777 ms per frame)
+        rank_samples = W * H * args.spp / world
+        n_streams = 2 if rank_samples >= 8e6 else 3
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
     shards = [TileShard(W, H, T, rank, world, dev, args.scheme) for _ in range(n_streams)]
     my_tiles = shards[0].tiles
