@@ -846,7 +846,10 @@ void trace_kernel(TraceParams P) {
             last_shadow = do_shadow;
         }
         // ---------------------------------------------------------- refill
-        uint64_t idle = do_shadow ? 0ull : __ballot(item < 0);
+        // me_idle: this lane's own bit of `idle` (kept as a lane predicate: testing the bit
+        // needs the 64-bit mask 1 << lane, which the register allocator spilled to scratch)
+        bool me_idle = !do_shadow && item < 0;
+        uint64_t idle = __ballot(me_idle);
         for (int round = 0; round < 2 && idle; ++round) {
             uint32_t avail = q_end - q_next;
             if (avail == 0 && !exhausted) {
@@ -863,7 +866,8 @@ void trace_kernel(TraceParams P) {
                     chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
                     // tiles hold >= 64 pixels (powers of two), so the chunk lies in one tile
                     uint32_t tk = (base - chunk_s * (uint32_t)P.n_slots) >> P.log_tpx;
-                    chunk_xy0 = __builtin_amdgcn_readfirstlane(P.tile_xy[tk]);
+                    // uniform index: a scalar load through the constant address space
+                    chunk_xy0 = ((const __attribute__((address_space(4))) uint32_t*)(uintptr_t)P.tile_xy)[tk];
                 }
                 avail = q_end - q_next;
             }
@@ -871,7 +875,7 @@ void trace_kernel(TraceParams P) {
             uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             uint32_t need = (uint32_t)__popcll(idle);
             uint32_t take = need < avail ? need : avail;
-            if (((idle >> lane) & 1ull) && rank < take) {
+            if (me_idle && rank < take) {
                 item = (int)(q_next + rank);
                 // start a new sample: main_taichi.py:89-95
                 L = v3(0, 0, 0);
@@ -904,7 +908,8 @@ void trace_kernel(TraceParams P) {
                 }
             }
             q_next += take;
-            idle = __ballot(item == -1);
+            me_idle = item == -1;
+            idle = __ballot(me_idle);
         }
         if (item == -2) item = -1;
         if (__ballot(item >= 0) == 0) {
