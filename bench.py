@@ -104,11 +104,12 @@ def load_scene(name):
     raise SystemExit(f"unknown scene {name}")
 
 
-def cpu_baseline(flat, cam, args):
+def cpu_sample(flat, cam, args, seconds):
     """Oracle (C restatement of PathTracer.trace, OpenMP) on a bounded sample of the
-    same workload: a subset of 8x8 tiles at the full spp/depth.  Closest hits by
-    stack traversal of the same BVH2 (oracle BACKEND_BVH, bit-identical to the
-    brute-force and reference-structure backends and the fastest of the three)."""
+    same workload: random 8x8 tiles of the frame at the full spp/depth, sized to about
+    `seconds` of CPU time.  Closest hits by stack traversal of the same BVH2 (oracle
+    BACKEND_BVH, bit-identical to the brute-force and reference-structure backends and
+    the fastest of the three).  Returns (tile ids, per-slot sums, seconds, threads)."""
     from oracle import oracle as O
     from pyrenderer_amd._native import Bvh
     osc = O.OracleScene.from_flat(flat)
@@ -124,17 +125,41 @@ def cpu_baseline(flat, cam, args):
     osc.render_tiles(cam, W, H, 8, 8, perm[:4], args.spp, args.depth, seed=args.seed, nthreads=cores,
                      backend=O.BACKEND_BVH)
     dt = max(time.perf_counter() - t0, 1e-3)
-    n = int(min(n_tiles_total, max(8, 4 * args.cpu_seconds / dt)))
+    n = int(min(n_tiles_total, max(8, 4 * seconds / dt)))
     ids = np.sort(perm[:n])
     t0 = time.perf_counter()
-    osc.render_tiles(cam, W, H, 8, 8, ids, args.spp, args.depth, seed=args.seed, nthreads=cores,
-                     backend=O.BACKEND_BVH)
+    sums = osc.render_tiles(cam, W, H, 8, 8, ids, args.spp, args.depth, seed=args.seed, nthreads=cores,
+                            backend=O.BACKEND_BVH)
     dt = time.perf_counter() - t0
+    return ids, sums, dt, cores
+
+
+def cpu_baseline(ids, dt, cores, args):
+    W = H = args.res
+    n = len(ids)
     samples = n * 64 * args.spp
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
             "sample": f"{n} random 8x8 tiles of the {W}x{H} frame at {args.spp} spp, depth {args.depth} "
                       f"({samples} samples, {dt:.1f} s); oracle/prt_oracle.c (C port of PathTracer.trace), "
                       f"BVH2 closest hit, OpenMP {cores} threads"}
+
+
+def l2_vs_cpu(gpu_sums, ids, cpu_sums, args):
+    """Per-pixel comparison of the timed frame (rank 0's gathered sums) with the CPU
+    oracle on the sampled 8x8 tiles: mean radiance = sums / spp on both sides; the
+    north-star tolerance is a per-pixel L2 < 1e-3."""
+    W = H = args.res
+    tx = W // 8
+    c = np.asarray(cpu_sums, np.float64).reshape(len(ids), 8, 8, 3)
+    g = np.stack([gpu_sums[(t % tx) * 8:(t % tx) * 8 + 8, (t // tx) * 8:(t // tx) * 8 + 8].transpose(1, 0, 2)
+                  for t in ids]).astype(np.float64)
+    diff = (g - c) / args.spp
+    pix_l2 = np.sqrt((diff ** 2).sum(axis=-1))
+    same = np.all(g.astype(np.float32) == c.astype(np.float32), axis=-1)
+    return {"pixels": int(pix_l2.size), "rmse": float(np.sqrt((diff ** 2).mean())),
+            "max_pixel_l2": float(pix_l2.max()), "identical_pixels": round(float(same.mean()), 6),
+            "tolerance": 1e-3, "pass": bool(pix_l2.max() < 1e-3),
+            "reference": "oracle/prt_oracle.c (C port of PathTracer.trace), same seed, random 8x8 tiles"}
 
 
 def main():
@@ -241,9 +266,15 @@ def main():
                     traffic = d.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline and rank == 0:
-            cpu = cpu_baseline(flat, cam, args)
+        cpu, l2 = None, None
+        if not args.no_cpu_baseline:
+            # at N = 1 the baseline sample (~cpu_seconds) doubles as the accuracy sample; at
+            # N > 1 only a short accuracy sample of the gathered frame is rendered on the CPU
+            ids, cpu_sums, dt, cores = cpu_sample(flat, cam, args, args.cpu_seconds if world == 1 else 2.0)
+            if world == 1:
+                cpu = cpu_baseline(ids, dt, cores, args)
+            torch.cuda.synchronize(dev)
+            l2 = l2_vs_cpu(shards[0].assemble(), ids, cpu_sums, args)
         line = {
             "metric": "Msamples/sec Cornell box 512²×64spp at 1/2/4/8 GPU; per-pixel L2 vs CPU",
             "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
@@ -269,6 +300,7 @@ def main():
                                 "ext_queries": round(ext / samples_per_step, 3),
                                 "shadow_queries": round(shadow / samples_per_step, 3)},
             "cpu_baseline": cpu,
+            "l2_vs_cpu": l2,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

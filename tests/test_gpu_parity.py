@@ -217,6 +217,28 @@ def test_frames_in_flight_on_two_streams(gpu_scene, oracle_scene, cornell):
         assert np.array_equal(outs[k].cpu().numpy().reshape(-1, 3), o), k
 
 
+def test_tile_set_changes_on_one_stream(gpu_scene, oracle_scene, cornell):
+    """A render context re-uploads its tile origins only when the tile set changes:
+    alternating tile sets (and sizes) on one stream must each match the oracle."""
+    import torch
+    from pyrenderer_amd.device_scene import interleaved_tiles
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    W, spp = 128, 4
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    sets = [(64, interleaved_tiles(W, W, 64, 0, 2)), (64, interleaved_tiles(W, W, 64, 1, 2)),
+            (32, interleaved_tiles(W, W, 32, 1, 3)), (64, interleaved_tiles(W, W, 64, 0, 2))]
+    outs = []
+    for tile, ids in sets:
+        buf = torch.empty(len(ids) * tile * tile * 3, dtype=torch.float32, device=dev)
+        gpu_scene.render_tiles_device(cam, W, W, tile, tile, ids, spp, 6, buf.data_ptr(), stream.cuda_stream, seed=4)
+        outs.append(buf)
+    torch.cuda.synchronize(dev)
+    for (tile, ids), buf in zip(sets, outs):
+        o = oracle_scene.render_tiles(cam, W, W, tile, tile, ids, spp, 6, seed=4)
+        assert np.array_equal(buf.cpu().numpy().reshape(-1, 3), o), (tile, list(ids))
+
+
 @pytest.mark.parametrize("mod", ["aperture", "projective"])
 def test_general_camera_matches_oracle(gpu_scene, oracle_scene, cornell, mod):
     """The kernel's pinhole/affine camera shortcut must not change a bit, and the
