@@ -569,7 +569,7 @@ template <bool STATS, int MODE, class S, bool QN = false, bool RES = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
                                              float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0,
-                                             int* fault = nullptr) {
+                                             int* fault = nullptr, int leaf_break = 0, int leaf_exit = 0) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     V3 oi = o * inv;
@@ -647,7 +647,9 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 cur = stk.get(sp);
                 --sp;
             }
-            if (!__any(leaf >= 0)) break;
+            // leave for the leaf phase once at most `leaf_break` of the lanes still
+            // descending have no postponed leaf (0: all of them hold one)
+            if (__popcll(__ballot(leaf >= 0)) <= (uint32_t)leaf_break) break;
         }
         while (leaf < 0) {
             int v = -leaf - 1;
@@ -671,6 +673,9 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 cur = stk.get(sp);
                 --sp;
             }
+            // back to the inner phase once at most `leaf_exit` lanes still hold a leaf
+            // (they keep it postponed); 0: drain every lane's chain of leaves first
+            if (__popcll(__ballot(leaf < 0)) <= (uint32_t)leaf_exit) break;
         }
         if (RES && (cur != kSentinel || leaf < 0) && __popcll(__ballot(true)) < min_lanes) break;
         // watchdog: a traversal revisiting nodes forever (corrupt tree) ends the query and
@@ -950,27 +955,27 @@ void trace_kernel(TraceParams P) {
             bool done;
             if (PHASE && do_shadow)
                 done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn,
-                                                                  &tst, P.resume_min, P.fault);
+                                                                  &tst, P.resume_min, P.fault, P.leaf_break, P.leaf_exit);
             else if (PHASE)
                 done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht,
-                                                                  cn, &tst, P.resume_min, P.fault);
+                                                                  cn, &tst, P.resume_min, P.fault, P.leaf_break, P.leaf_exit);
             else
                 done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk,
-                                                                  hid, ht, cn, &tst, P.resume_min, P.fault);
+                                                                  hid, ht, cn, &tst, P.resume_min, P.fault, P.leaf_break, P.leaf_exit);
             pending = !done;
             if (pending) continue;   // resume next iteration; no shading yet
             hit = hid >= 0;
         } else if (TRAV == 3 && PHASE) {
-            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn, nullptr, 0, P.fault);
-            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn, nullptr, 0, P.fault);
+            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
+            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
         } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
         } else {
             park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
             park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
             park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
             asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
             asm volatile("" ::: "memory");
             float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
             beta = v3(k0.x, k0.y, k0.z);

@@ -22,6 +22,8 @@ struct TraceParams {
     // evaluated on the host in the kernel's f32 order (camera_taichi.py:47-74)
     int cam_fast;
     int* fault;               // watchdog flag (non-zero: a traversal exceeded kGuardTrips)
+    int leaf_break;           // while-while: enter the leaf phase when <= this many descending lanes lack a leaf
+    int leaf_exit;            // ... and leave it when <= this many lanes still hold a leaf
     int resume_min;           // resume variants: leave the traversal loop below this many active lanes
     int* spill;               // spill variants: per-lane stack entries beyond the LDS part (stride = grid threads)
     const float4* rays;       // primary rays of this launch from camera_kernel, or null (generated in the refill)

@@ -1,7 +1,8 @@
-"""A/B the BVH builder's knobs (env PRT_SAH_CT, PRT_SAH_BINS, PRT_LEAF_MIN, PRT_MAX_LEAF)
-on one device: one scene build per setting, interleaved timed rounds, counted work per
-sample, and a check that every setting renders the identical image (closest hits do
-not depend on the tree).
+"""A/B the scene-creation knobs (env PRT_SAH_CT, PRT_SAH_BINS, PRT_LEAF_MIN, PRT_MAX_LEAF,
+PRT_LEAF_BREAK, PRT_RESUME_MIN) on one device: one scene per setting, interleaved timed
+rounds of `--launches` device-resident frames each (HIP-event kernel time), counted work
+per sample, and a check that every setting renders the identical image (closest hits do
+not depend on the tree or the traversal schedule).
 
     python tools/bvh_knobs.py --config 2 --settings "" "PRT_SAH_CT=1" "PRT_MAX_LEAF=8,PRT_LEAF_MIN=1"
 """
@@ -14,7 +15,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-KNOBS = ("PRT_SAH_CT", "PRT_SAH_BINS", "PRT_LEAF_MIN", "PRT_MAX_LEAF")
+KNOBS = ("PRT_SAH_CT", "PRT_SAH_BINS", "PRT_LEAF_MIN", "PRT_MAX_LEAF", "PRT_LEAF_BREAK", "PRT_LEAF_EXIT", "PRT_RESUME_MIN")
 
 
 def apply(setting):
@@ -30,6 +31,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--launches", type=int, default=5, help="timed frames per setting per round")
     ap.add_argument("--settings", nargs="+", default=[""])
     a = ap.parse_args()
     import bench
@@ -48,12 +50,20 @@ def main():
         apply(s)
         scenes[s] = DeviceScene(flat, 0)
         res[s] = []
+    import torch
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    buf = torch.empty(len(ids) * 64 * 64 * 3, dtype=torch.float32, device=dev)
     for r in range(a.rounds + 1):
         for s in a.settings:
             apply(s)
-            out, _ = scenes[s].render_tiles(cam, W, H, 64, 64, ids, cfg["spp"], cfg["depth"], 0,
-                                            PRT_FLAG_TIME | (a.variant << 8))
+            scenes[s].kernel_timing()
+            for _ in range(a.launches):
+                scenes[s].render_tiles_device(cam, W, H, 64, 64, ids, cfg["spp"], cfg["depth"], buf.data_ptr(),
+                                              stream.cuda_stream, flags=PRT_FLAG_TIME | (a.variant << 8))
+            torch.cuda.synchronize(dev)
             ms, n = scenes[s].kernel_timing()
+            out = buf.cpu().numpy()
             if ref is None:
                 ref = out
             if r > 0:
