@@ -15,7 +15,7 @@ PRT_FLAG_STATS = 0x1
 PRT_FLAG_TIME = 0x2
 PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
 # trace-kernel variant ids 1..VAR_LAST (pyrenderer_amd/csrc/prt_kernels.h)
-VAR_LAST = 30
+VAR_LAST = 31
 VAR_WW4_PH_LDS6 = 15
 VAR_WW4_Q_SP5 = 23
 PRT_HITS_ANY = 0x1

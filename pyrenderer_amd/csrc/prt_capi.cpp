@@ -239,8 +239,9 @@ bool lds_fits4(const Scene* s) { return lds_fits_var(s, true); }
 // LDS-resident scene when it fits; the >= 6 waves/SIMD build when six blocks' LDS
 // still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
 int default_variant(const Scene* s) {
-    // global scene: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal tails
-    if (!lds_fits4(s)) return prt::kVarWW4QRSp5;
+    // global scene: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal
+    // tails, >= 6 waves/SIMD (C4: 28.6 ms at 5 waves, 27.2 at 6, 28.6 at 7 with spills)
+    if (!lds_fits4(s)) return prt::kVarWW4QRSp6;
     if (!s->stack4) return prt::kVarWW;
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));

@@ -1219,7 +1219,8 @@ void trace_kernel(TraceParams P) {
     X(kVarWW4RLds6, 131, true, 6)                        \
     X(kVarWW4QRSp5, 227, false, 5)                       \
     X(kVarWW4PhLds7, 11, true, 7)                        \
-    X(kVarWW4PhLds5, 11, true, 5)
+    X(kVarWW4PhLds5, 11, true, 5)                        \
+    X(kVarWW4QRSp6, 227, false, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>

@@ -79,7 +79,8 @@ constexpr int kVarWW4RLds6 = 27;    // resume, mixed schedule, LDS scene, >= 6 w
 constexpr int kVarWW4QRSp5 = 28;    // resume, quantised nodes, spill stack, >= 5 waves
 constexpr int kVarWW4PhLds7 = 29;   // phase-aligned, LDS scene, >= 7 waves per SIMD
 constexpr int kVarWW4PhLds5 = 30;   // ... >= 5 waves per SIMD
-constexpr int kVarLast = 30;
+constexpr int kVarWW4QRSp6 = 31;   // resume, quantised nodes, spill stack, >= 6 waves per SIMD
+constexpr int kVarLast = 31;
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
 bool variant_quantized(int var);
