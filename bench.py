@@ -7,7 +7,8 @@ buffer, then the per-tile radiance sums are gathered to rank 0 over RCCL
 (torch.distributed 'nccl' backend).  Total work is fixed as N grows ("scaling":
 "strong").  Consecutive frames alternate between --streams HIP streams, each with
 its own buffers, so the drain of frame k (the last paths of a persistent launch,
-~0.3 ms at any frame size) and its gather overlap the start of frame k+1.
+~0.3 ms at any frame size) and its gather overlap the start of frame k+1 (auto: 3
+streams when a rank renders < 8 M samples per frame, else serial frames).
 
     python bench.py --gpus 1 --steps 10 --warmup 3
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
@@ -76,15 +77,16 @@ def parse():
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--tile", type=int, default=64)
     ap.add_argument("--streams", type=int, default=0,
-                    help="frames in flight (1 = strictly serial frames; 0 = auto: 2, or 3 when a rank renders "
+                    help="frames in flight (1 = strictly serial frames; 0 = auto: 1, or 3 when a rank renders "
                          "< 8 M samples per frame, where the launch tail is a larger share)")
     ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per trace launch (tools/pmc_traffic.py); null if absent")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc.json"),
+                    help="PMC summaries per workload (tools/pmc_summary.py): HBM bytes per trace launch, "
+                         "VALU issue / lane utilisation; traffic is null for a workload without an entry")
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
@@ -193,10 +195,14 @@ def main():
     T = args.tile
     n_streams = args.streams
     if n_streams <= 0:
-        # measured (profiles/r01/shard_sim_*): 2 frames in flight are best for a whole C2 frame
-        # on one GPU, 3 for the 1/8 frame of an 8-rank run (0.741 vs 0.777 ms per frame)
+        # measured (profiles/r01/shard_sim_*, streams_ab): for a whole C2 frame on one GPU,
+        # overlapping frames gains ~2 % (5.15 vs 5.26 ms) but makes every launch's event span
+        # include time shared with the next frame, so the roofline's kernel duration (and the
+        # rocprof average it is checked against) would no longer be the kernel's own; serial
+        # frames keep them equal.  For the 1/4 and 1/8 frames of 4- and 8-rank runs the launch
+        # tail is a larger share: 3 frames in flight (0.741 vs 0.777 ms per frame at 1/8).
         rank_samples = W * H * args.spp / world
-        n_streams = 2 if rank_samples >= 8e6 else 3
+        n_streams = 1 if rank_samples >= 8e6 else 3
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
     shards = [TileShard(W, H, T, rank, world, dev, args.scheme) for _ in range(n_streams)]
     my_tiles = shards[0].tiles
@@ -257,15 +263,13 @@ def main():
                         + B_SAMPLE * n_px_rank * args.spp + B_PIXEL * n_px_rank) / launches_per_step
         achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
         flops_launch = (F_BOX * arity * nodes + F_TRI * tris) * per_rank / launches_per_step
-        traffic = None
-        tj = args.traffic_json
-        if tj and os.path.exists(tj):
+        traffic, pmc = None, {}
+        if args.pmc_json and os.path.exists(args.pmc_json) and world == 1:
             try:
-                d = json.load(open(tj))
-                if d.get("config") == f"{args.scene}_{W}x{H}x{args.spp}spp_d{args.depth}" and world == 1:
-                    traffic = d.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+                pmc = json.load(open(args.pmc_json)).get(f"{args.scene}_{W}x{H}x{args.spp}spp_d{args.depth}", {})
+            except (OSError, ValueError):
+                pmc = {}
+            traffic = pmc.get("hbm_bytes_per_launch")
         cpu, l2 = None, None
         if not args.no_cpu_baseline:
             # at N = 1 the baseline sample (~cpu_seconds) doubles as the accuracy sample; at
@@ -295,7 +299,11 @@ def main():
                          "note": "achieved = logical scene + sample-buffer bytes (DESIGN.md §5); small scenes "
                                  "are served from LDS, so frac may exceed 1; traffic = PMC HBM bytes per launch"},
             "valu": {"achieved_tflops": round(flops_launch / (kern_avg_ms * 1e-3) / 1e12, 2),
-                     "peak_tflops": VALU_PEAK_TFLOPS},
+                     "peak_tflops": VALU_PEAK_TFLOPS,
+                     "issue_util": pmc.get("valu_issue_util"), "lane_util": pmc.get("valu_lane_util"),
+                     "note": "achieved = counted box/triangle flops; issue_util / lane_util from the committed "
+                             "SQ counter pass (profiles/pmc.json): the kernel is bound by VALU issue under "
+                             "divergence, not by HBM"},
             "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),
                                 "ext_queries": round(ext / samples_per_step, 3),
                                 "shadow_queries": round(shadow / samples_per_step, 3)},
