@@ -53,10 +53,37 @@ __device__ __forceinline__ V3 cross(V3 a, V3 b) {
 __device__ __forceinline__ bool div_is_nan(float a, float b) {
     return isnan(a) || isnan(b) || (a == 0.0f && b == 0.0f) || (isinf(a) && isinf(b));
 }
+// (a.x / b, a.y / b, a.z / b), correctly rounded like IEEE division.  The compiler's
+// expansion of one f32 division on gfx950 is
+//     v_div_scale (den), v_rcp, 2 fma (reciprocal refinement), v_div_scale (num), mul,
+//     3 fma (two quotient corrections, the last as v_div_fmas), v_div_fixup
+// and v_div_scale / v_div_fixup change nothing when numerator and denominator are finite
+// with |x| in [2^-40, 2^40]: the exponent difference (<= 80) stays below the scaling
+// threshold of 96, the denominator, its reciprocal and the quotient are normal, and the
+// numerator's biased exponent exceeds 23.  For such operands the remaining sequence
+// is therefore bit-identical to the full expansion, and the reciprocal refinement is
+// shared by the three quotients of one denominator.  A wave with any lane outside the
+// range (zero, tiny, huge, inf, NaN) takes the plain divisions.
+__device__ __forceinline__ V3 div3(V3 a, float b) {
+    // fminf drops a NaN operand, the sum does not: a NaN or inf anywhere fails `sum <= 2^40`
+    const float lo = fminf(fminf(fabsf(a.x), fabsf(a.y)), fminf(fabsf(a.z), fabsf(b)));
+    const float sum = (fabsf(a.x) + fabsf(a.y)) + (fabsf(a.z) + fabsf(b));
+    const bool ok = lo >= 0x1p-40f && sum <= 0x1p40f;
+    if (__ballot(!ok) == 0) {
+        float r = __builtin_amdgcn_rcpf(b);
+        r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+        auto q1 = [&](float n) {
+            float q = n * r;
+            q = __builtin_fmaf(__builtin_fmaf(-b, q, n), r, q);
+            return __builtin_fmaf(__builtin_fmaf(-b, q, n), r, q);
+        };
+        return v3(q1(a.x), q1(a.y), q1(a.z));
+    }
+    return v3(a.x / b, a.y / b, a.z / b);
+}
 // taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt)
 __device__ __forceinline__ V3 normalize(V3 a) {
-    float l = sqrtf(dot(a, a));
-    return v3(a.x / l, a.y / l, a.z / l);
+    return div3(a, sqrtf(dot(a, a)));
 }
 __device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
 
@@ -97,17 +124,16 @@ __device__ __forceinline__ V3 cosine_hemisphere(float u0, float u1) {
     float ox = 2.0f * u0 - 1.0f, oy = 2.0f * u1 - 1.0f;
     float dx = 0.0f, dy = 0.0f;
     if (!(ox == 0.0f && oy == 0.0f)) {
-        float r, c, s;
-        if (fabsf(ox) > fabsf(oy)) {
-            r = ox;
-            float th = kPiOver4 * (oy / ox);
-            c = poly_cos(th); s = poly_sin(th);
-        } else {
-            r = oy;
-            float a = kPiOver4 * (ox / oy);   // theta = pi/2 - a
-            c = poly_sin(a); s = poly_cos(a);
-        }
-        dx = r * c; dy = r * s;
+        // |ox| > |oy|: r = ox, theta = pi/4 (oy/ox), (c, s) = (cos, sin)(theta);
+        // else:        r = oy, a = pi/4 (ox/oy), theta = pi/2 - a, (c, s) = (sin, cos)(a).
+        // Both cases as one division and one polynomial pair on selected operands (a
+        // divergent if/else would run two of each on a wave holding both cases).
+        const bool wide = fabsf(ox) > fabsf(oy);
+        const float r = wide ? ox : oy;
+        const float t = kPiOver4 * ((wide ? oy : ox) / r);
+        const float pc = poly_cos(t), ps = poly_sin(t);
+        dx = r * (wide ? pc : ps);
+        dy = r * (wide ? ps : pc);
     }
     float m = 1.0f - dx * dx - dy * dy;
     return v3(dx, dy, sqrtf(m > 0.0f ? m : 0.0f));
@@ -1095,7 +1121,8 @@ void trace_kernel(TraceParams P) {
                     // exactly when a / pdf is, so the condition is decided before dividing.
                     V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
                     if (div_is_nan(ad.x, pdf) || div_is_nan(ad.y, pdf) || div_is_nan(ad.z, pdf)) pdf = 1e-4f;
-                    V3 nb = v3(ad.x / pdf * kInvPi, ad.y / pdf * kInvPi, ad.z / pdf * kInvPi);
+                    V3 adp = div3(ad, pdf);
+                    V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
                     beta = beta * nb;
                     // sample_direct_lighting (tracing.py:92-108)
                     int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
@@ -1122,7 +1149,7 @@ void trace_kernel(TraceParams P) {
                         const float* em = s_mats + 8 * __float_as_int(LN.w);
                         V3 dd = p - p2;
                         float sl = dot(dd, dd);
-                        V3 rad = v3(em[0] * dot1 * dot2 / sl, em[1] * dot1 * dot2 / sl, em[2] * dot1 * dot2 / sl);
+                        V3 rad = div3(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl);
                         pend = beta * rad;
                         d = w;
                         tmax = t_at;
