@@ -81,6 +81,19 @@ __device__ __forceinline__ V3 div3(V3 a, float b) {
     }
     return v3(a.x / b, a.y / b, a.z / b);
 }
+// 1 / b, correctly rounded: for finite |b| in [2^-40, 2^40] the division expansion (see
+// div3) with numerator 1 is the refined reciprocal plus two quotient corrections
+// (its q = 1 * r is exact); other waves take the plain division.
+__device__ __forceinline__ float rcp_exact(float b) {
+    const float ab = fabsf(b);
+    if (__ballot(!(ab >= 0x1p-40f && ab <= 0x1p40f)) == 0) {
+        float r = __builtin_amdgcn_rcpf(b);
+        r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+        const float q = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+        return __builtin_fmaf(__builtin_fmaf(-b, q, 1.0f), r, q);
+    }
+    return 1.0f / b;
+}
 // taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt)
 __device__ __forceinline__ V3 normalize(V3 a) {
     return div3(a, sqrtf(dot(a, a)));
@@ -270,7 +283,7 @@ __device__ __forceinline__ bool mt(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, fl
     V3 c = cross(e1, d);
     float det = dot(c, e2);
     if (!(fabsf(det) > 0.0f)) return false;
-    float f = 1.0f / det;
+    float f = rcp_exact(det);
     V3 s = o - v0;
     V3 q = cross(s, e2);
     float t = -f * dot(q, e1);
@@ -352,7 +365,7 @@ __device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, 
     V3 c = cross(e1, d);
     float det = dot(c, e2);
     if (!(fabsf(det) > 0.0f)) return false;
-    float f = 1.0f / det;
+    float f = rcp_exact(det);
     V3 s = o - v0;
     V3 q = cross(s, e2);
     float t = -f * dot(q, e1);
