@@ -362,21 +362,22 @@ __device__ __forceinline__ bool traverse(const TraceParams& P, V3 o, V3 d, float
 // small scene (the compiler infers the address space after inlining).
 __device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, float tbest, int id, int best_id,
                                      bool any, float& tout) {
+    // branch-free: a lane failing an early test would wait for the wave's other lanes
+    // anyway, so every value is computed and the tests are combined (same results as the
+    // reference's early returns; det == 0 is rejected, its quotient never used)
     V3 c = cross(e1, d);
     float det = dot(c, e2);
-    if (!(fabsf(det) > 0.0f)) return false;
-    float f = rcp_exact(det);
+    const bool nz = fabsf(det) > 0.0f;
+    float f = rcp_exact(nz ? det : 1.0f);
     V3 s = o - v0;
     V3 q = cross(s, e2);
     float t = -f * dot(q, e1);
-    bool in_range = t0 < t && (t < tbest || (!any && t == tbest && id < best_id));
-    if (!in_range) return false;
     float u = -f * dot(q, d);
-    if (!(0.0f <= u && u <= 1.0f)) return false;
     float v = f * dot(c, s);
-    if (!(v >= 0.0f && 1.0f - u - v >= 0.0f)) return false;
+    const bool in_range = t0 < t && (t < tbest || (!any && t == tbest && id < best_id));
+    const bool hit = nz & in_range & (0.0f <= u) & (u <= 1.0f) & (v >= 0.0f) & (1.0f - u - v >= 0.0f);
     tout = t;
-    return true;
+    return hit;
 }
 
 template <bool STATS>
