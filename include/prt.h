@@ -117,6 +117,16 @@ void prt_scene_destroy(void* scene);
 int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th,
                      const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
                      uint32_t flags, float* out_sum, uint64_t* stats);
+/* Progressive rendering: main_taichi.py:108-127 runs render() once per GUI frame
+ * (pixels[x,y] += L, samples[x,y] += 1) and displays the running mean.  This call
+ * renders samples first_sample .. first_sample+spp-1 of every pixel (the same
+ * (seed, pixel, sample) random streams as prt_render_tiles) and adds them, in
+ * sample order, onto io_sum (host, n_tiles*tw*th x 3 f32, same slot order):
+ * calls covering samples [0, a), [a, b), ... leave io_sum bit-identical to one
+ * prt_render_tiles call of b samples.  Synchronous. */
+int prt_render_tiles_accumulate(void* scene, const float* cam, int W, int H, int tw, int th,
+                                const int32_t* tile_ids, int n_tiles, int first_sample, int spp, int depth,
+                                uint64_t seed, uint32_t flags, float* io_sum);
 /* Same work, result left in device memory `d_out_sum` (n_slots x 3 f32) and
  * enqueued on `stream` (a hipStream_t; NULL = the scene's own stream) without
  * a host synchronisation. tile_ids is a host array.  The scene keeps one set of

@@ -52,6 +52,7 @@ EXPORTS = {
     "prt_scene_destroy": (None, [_vp]),
     "prt_render_tiles": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
+    "prt_render_tiles_accumulate": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_kernel_timing": (_i, [_vp, _vp, _vp]),
     "prt_last_stats": (_i, [_vp, _vp]),
     "prt_diag_stats": (_i, [_vp, _vp]),

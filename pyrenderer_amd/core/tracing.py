@@ -12,6 +12,10 @@ estimator in the HIP kernel (pyrenderer_amd/csrc/prt_kernels.hip).
 (tile id % n_devices); the image is bit-identical for any device count since
 random numbers are keyed by (seed, global pixel, sample).  For one process per
 GPU use pyrenderer_amd.distributed (RCCL gather over xGMI).
+
+`Accumulator` is the progressive form of main_taichi.py:108-127 (render() once
+per GUI frame, pixels += L, samples += 1, finish() of the running mean), with
+save / load to resume an accumulation.
 """
 import threading
 
@@ -88,6 +92,67 @@ def render(scene, camera, *, spp, depth, seed=0, resolution=None, devices=(0,), 
     world = world or build_world(scene, devices)
     tracer = PathTracer(world, depth, int(W), int(H))
     return tracer.render(camera.convert_to_taichi_camera().packed(), spp, seed, devices, tile)
+
+
+class Accumulator:
+    """Progressive rendering on one device (main_taichi.py:108-127).
+
+    `add(spp)` renders the next `spp` samples of every pixel and adds them in sample
+    order onto the running per-pixel sums, so any split of N samples over add() calls
+    leaves the sums bit-identical to `render(spp=N)` * N.  `mean()` is
+    pixels / samples (main_taichi.py:61-64, before the sqrt tone map).  `save(path)` /
+    `Accumulator.load(path, scene, camera)` resume an accumulation (.npz: sums, sample
+    count, seed, depth, resolution, tile).
+    """
+
+    def __init__(self, scene, camera, *, depth, seed=0, resolution=None, device=0, tile=64, world=None):
+        W, H = resolution if resolution is not None else camera.resolution
+        self.W, self.H, self.depth, self.seed, self.tile = int(W), int(H), int(depth), int(seed), int(tile)
+        self.device = device
+        self.world = world or build_world(scene, (device,))
+        self.cam = camera.convert_to_taichi_camera().packed()
+        self.ids = interleaved_tiles(self.W, self.H, self.tile)
+        self.slots = np.zeros((self.ids.shape[0] * self.tile * self.tile, 3), np.float32)
+        self.samples = 0
+
+    def add(self, spp=1):
+        """Render samples [samples, samples + spp) of every pixel onto the sums."""
+        if spp < 0:
+            raise ValueError("spp must be >= 0")
+        ds = self.world.device_scene(self.device)
+        ds.render_tiles_accumulate(self.cam, self.W, self.H, self.tile, self.tile, self.ids, self.samples, spp,
+                                   self.depth, self.slots, self.seed)
+        self.samples += spp
+        return self
+
+    def sums(self):
+        """Per-pixel radiance sums (W, H, 3) [x][y] — the reference's `pixels` field."""
+        return unpack_tiles(self.slots, self.W, self.H, self.tile, self.tile, self.ids)
+
+    def mean(self):
+        if self.samples == 0:
+            return np.zeros((self.W, self.H, 3), np.float32)
+        return self.sums() / np.float32(self.samples)
+
+    def state(self):
+        return dict(slots=self.slots, samples=np.int64(self.samples), seed=np.int64(self.seed),
+                    depth=np.int64(self.depth), resolution=np.array([self.W, self.H], np.int64),
+                    tile=np.int64(self.tile))
+
+    def save(self, path):
+        np.savez(path, **self.state())
+
+    @classmethod
+    def load(cls, path, scene, camera, device=0, world=None):
+        z = np.load(path, allow_pickle=False)
+        W, H = (int(v) for v in z["resolution"])
+        acc = cls(scene, camera, depth=int(z["depth"]), seed=int(z["seed"]), resolution=(W, H), device=device,
+                  tile=int(z["tile"]), world=world)
+        if z["slots"].shape != acc.slots.shape:
+            raise ValueError("saved accumulation does not match the frame layout")
+        acc.slots[...] = z["slots"]
+        acc.samples = int(z["samples"])
+        return acc
 
 
 def as_image(radiance_xy):

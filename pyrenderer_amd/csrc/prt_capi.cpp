@@ -258,9 +258,12 @@ bool camera_is_fast(const float* cam) {
     return fin && !(cam[19] > 0.0f) && cam[12] == 0.0f && cam[13] == 0.0f && cam[14] == 0.0f && cam[15] == 1.0f;
 }
 
-// Enqueue the whole render of a tile set on `stream`, result in d_acc.
+// Enqueue the whole render of a tile set on `stream`, result in d_acc: samples
+// first_sample .. first_sample + spp - 1 of every pixel; `accumulate` adds them onto the
+// sums already in d_acc (progressive rendering) instead of overwriting them.
 int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
-                   int n_tiles, int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc) {
+                   int n_tiles, int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc,
+                   int first_sample = 0, bool accumulate = false) {
     const int64_t n_slots = (int64_t)n_tiles * tw * th;
     if (n_slots == 0) return PRT_OK;
     hipStream_t stream = cx->stream;
@@ -279,7 +282,8 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         cx->tile_host.swap(origins);
     }
     if (spp == 0 || depth == 0) {
-        HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots, stream));
+        // every sample's radiance is 0: the sums are 0, or unchanged when accumulating
+        if (!accumulate) HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots, stream));
         return PRT_OK;
     }
     // per-sample buffers: radiance (12 B) + primary ray (16 B, pinhole cameras)
@@ -381,7 +385,7 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     }
     for (int64_t s0 = 0; s0 < spp; s0 += chunk, ++k) {
         int64_t n = std::min<int64_t>(chunk, spp - s0);
-        P.s0 = (int)s0;
+        P.s0 = first_sample + (int)s0;   // global sample index: keys the RNG streams
         P.n_items = (uint64_t)(n * n_slots);
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
@@ -390,7 +394,8 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
         HIP_TRY(prt::launch_trace(P, stack, var, grid, stats, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k + 1], stream));
-        HIP_TRY(prt::launch_reduce((const float*)cx->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0, stream));
+        HIP_TRY(prt::launch_reduce((const float*)cx->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0 && !accumulate,
+                                   stream));
     }
     return PRT_OK;
 }
@@ -655,6 +660,33 @@ int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th
             std::memset(stats, 0, 4 * sizeof(uint64_t));
         }
     }
+    return PRT_OK;
+}
+
+int prt_render_tiles_accumulate(void* scene, const float* cam, int W, int H, int tw, int th,
+                                const int32_t* tile_ids, int n_tiles, int first_sample, int spp, int depth,
+                                uint64_t seed, uint32_t flags, float* io_sum) {
+    auto* s = (Scene*)scene;
+    int rc = check_render_args(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth);
+    if (rc) return rc;
+    if (!io_sum && n_tiles > 0) return fail(PRT_ERR_ARG, "io_sum is NULL");
+    if (first_sample < 0 || (int64_t)first_sample + spp > INT32_MAX)
+        return fail(PRT_ERR_ARG, "first_sample must be >= 0 and first_sample + spp < 2^31");
+    DeviceGuard g(s->device);
+    const int64_t n_slots = (int64_t)n_tiles * tw * th;
+    if (n_slots == 0) return PRT_OK;
+    RenderCtx* cx = ctx_for(s, s->stream);
+    if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
+    const size_t bytes = sizeof(float) * 3 * (size_t)n_slots;
+    HIP_TRY(cx->acc.ensure(std::max<size_t>(16, bytes)));
+    HIP_TRY(hipMemcpyAsync(cx->acc.p, io_sum, bytes, hipMemcpyHostToDevice, s->stream));
+    if ((rc = enqueue_render(s, cx, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, (float*)cx->acc.p,
+                             first_sample, true)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(io_sum, cx->acc.p, bytes, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (read_fault_at(cx->work) != 0)
+        return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     return PRT_OK;
 }
 

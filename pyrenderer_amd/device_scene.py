@@ -103,6 +103,18 @@ class DeviceScene:
                                          depth, int(seed), flags, N.ptr(out), N.ptr(stats)))
         return out, stats
 
+    def render_tiles_accumulate(self, cam, W, H, tw, th, tile_ids, first_sample, spp, depth, sums, seed=0, flags=0):
+        """Progressive rendering: add samples first_sample .. first_sample+spp-1 onto `sums`
+        ((n_tiles*tw*th, 3) float32, modified in place, slot order of render_tiles)."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        tile_ids = np.ascontiguousarray(tile_ids, np.int32)
+        if sums.dtype != np.float32 or not sums.flags.c_contiguous or sums.shape != (tile_ids.shape[0] * tw * th, 3):
+            raise ValueError("sums must be a C-contiguous float32 (n_tiles*tw*th, 3) array")
+        N.check(N.lib().prt_render_tiles_accumulate(self.h, N.ptr(cam), W, H, tw, th, N.ptr(tile_ids),
+                                                    tile_ids.shape[0], int(first_sample), spp, depth, int(seed), flags,
+                                                    N.ptr(sums)))
+        return sums
+
     def render_tiles_device(self, cam, W, H, tw, th, tile_ids, spp, depth, d_out_ptr, stream_ptr=None, seed=0,
                             flags=0):
         """Enqueue; result stays in device memory at d_out_ptr (n_slots x 3 f32)."""

@@ -217,6 +217,28 @@ def test_frames_in_flight_on_two_streams(gpu_scene, oracle_scene, cornell):
         assert np.array_equal(outs[k].cpu().numpy().reshape(-1, 3), o), k
 
 
+def test_progressive_accumulation_matches_one_render(cornell, oracle_scene, tmp_path):
+    """Accumulator (main_taichi.py's progressive loop): samples added over several calls,
+    across a save / load, give the sums of one render of all samples, bit for bit."""
+    from pyrenderer_amd.core.tracing import Accumulator, render
+    scene, camera, _ = cornell
+    W, H, depth, seed = 96, 64, 6, 11
+    acc = Accumulator(scene, camera, depth=depth, seed=seed, resolution=(W, H))
+    acc.add(2).add(3).add(0).add(1)
+    assert acc.samples == 6
+    cam = camera.convert_to_taichi_camera().packed()
+    o6 = oracle_scene.render(cam, W, H, 6, depth, seed=seed)
+    assert np.array_equal(acc.sums(), o6)
+    assert np.array_equal(acc.mean(), render(scene, camera, spp=6, depth=depth, seed=seed, resolution=(W, H),
+                                             world=acc.world))
+    path = str(tmp_path / "acc.npz")
+    acc.save(path)
+    resumed = Accumulator.load(path, scene, camera, world=acc.world)
+    resumed.add(2)
+    assert resumed.samples == 8
+    assert np.array_equal(resumed.sums(), oracle_scene.render(cam, W, H, 8, depth, seed=seed))
+
+
 def test_tile_set_changes_on_one_stream(gpu_scene, oracle_scene, cornell):
     """A render context re-uploads its tile origins only when the tile set changes:
     alternating tile sets (and sizes) on one stream must each match the oracle."""
