@@ -117,6 +117,29 @@ void prt_scene_destroy(void* scene);
 int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th,
                      const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
                      uint32_t flags, float* out_sum, uint64_t* stats);
+/* One rectangular window of the frame, as SURVEY.md §8(b)'s prt_render: samples
+ * 0..spp-1 of the pixels [x0, x0+w) x [y0, y0+h) of a W x H frame (random streams
+ * keyed by the global pixel, so any window equals the same crop of a full-frame render),
+ * path depth `depth`.  out_sum: w x h x 3 f32, the per-pixel radiance SUM over samples
+ * in sample order, indexed [x - x0][y - y0] like the reference's pixels.to_numpy()
+ * (main_taichi.py:25, the render() kernel of main_taichi.py:80-99 run spp times).
+ * Rendered as the 8 x 8 tiles covering the window.  stats as prt_render_tiles. */
+int prt_render(void* scene, const float* cam, int W, int H, int x0, int y0, int w, int h, int spp, int depth,
+               uint64_t seed, uint32_t flags, float* out_sum, uint64_t* stats);
+/* The whole W x H frame over several GPUs of this process (SURVEY.md §8(b)
+ * prt_render_multi, §8(e)): scenes[r] is a scene handle on its own device (all
+ * distinct; scenes[0] is the root).  Tiles of tile x tile pixels go to rank
+ * (tx + s*ty) mod n_scenes (the 'latin' interleave of device_scene.tile_owner), every
+ * rank renders its tiles on its device, and ONE RCCL group of ncclSend (each rank,
+ * the root included) / ncclRecv (root) moves the packed tile sums to the root over
+ * xGMI, where they are scattered into out_frame (host, W x H x 3 f32 sums, [x][y]).
+ * Bit-identical to prt_render / prt_render_tiles of the same frame for any n_scenes.
+ * The communicator (ncclCommInitAll over the scenes' devices) is created on first use
+ * and cached per device list; prt_comm_release() destroys the cached ones.  librccl
+ * is loaded at first use: PRT_ERR_RCCL when it is missing.  Synchronous. */
+int prt_render_multi(void* const* scenes, int n_scenes, const float* cam, int W, int H, int tile, int spp, int depth,
+                     uint64_t seed, uint32_t flags, float* out_frame);
+void prt_comm_release(void);
 /* Progressive rendering: main_taichi.py:108-127 runs render() once per GUI frame
  * (pixels[x,y] += L, samples[x,y] += 1) and displays the running mean.  This call
  * renders samples first_sample .. first_sample+spp-1 of every pixel (the same

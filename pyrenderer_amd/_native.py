@@ -51,6 +51,9 @@ EXPORTS = {
     "prt_closest_hits": (_i, [_vp, _vp, ctypes.c_int64, _u32, _vp, _vp]),
     "prt_scene_destroy": (None, [_vp]),
     "prt_render_tiles": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
+    "prt_render": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _u64, _u32, _vp, _vp]),
+    "prt_render_multi": (_i, [_vp, _i, _vp, _i, _i, _i, _i, _i, _u64, _u32, _vp]),
+    "prt_comm_release": (None, []),
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_tiles_accumulate": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_kernel_timing": (_i, [_vp, _vp, _vp]),

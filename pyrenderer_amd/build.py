@@ -67,7 +67,7 @@ def build(force=False, verbose=False):
         if verbose and (r.stderr or r.stdout).strip():
             print(r.stdout + r.stderr, flush=True)
     tmp = LIB + ".tmp"
-    link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + [obj for _, obj, _ in units]
+    link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + [obj for _, obj, _ in units] + ["-ldl"]
     if verbose:
         print(" ".join(link), flush=True)
     subprocess.check_call(link)

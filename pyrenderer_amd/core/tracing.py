@@ -9,19 +9,19 @@ reference's `pixels.to_numpy()`.  Every sample runs PathTracer.trace's
 estimator in the HIP kernel (pyrenderer_amd/csrc/prt_kernels.hip).
 
 `devices=(0, 1, ...)` shards 64x64 tiles across GPUs of this process
-(tile id % n_devices); the image is bit-identical for any device count since
-random numbers are keyed by (seed, global pixel, sample).  For one process per
-GPU use pyrenderer_amd.distributed (RCCL gather over xGMI).
+('latin' interleave, device_scene.tile_owner) through prt_render_multi, which
+gathers the tile sums to the first device with one RCCL send/recv group; the
+image is bit-identical for any device count since random numbers are keyed by
+(seed, global pixel, sample).  For one process per GPU use
+pyrenderer_amd.distributed (torch.distributed gather over RCCL/xGMI).
 
 `Accumulator` is the progressive form of main_taichi.py:108-127 (render() once
 per GUI frame, pixels += L, samples += 1, finish() of the running mean), with
 save / load to resume an accumulation.
 """
-import threading
-
 import numpy as np
 
-from ..device_scene import interleaved_tiles, unpack_tiles
+from ..device_scene import interleaved_tiles, render_multi, unpack_tiles
 from ..mathematics.intersection import World
 
 
@@ -38,36 +38,14 @@ class PathTracer:
     def render_sums(self, cam_packed, spp, seed=0, devices=(0,), tile=64, flags=0):
         """Per-pixel radiance SUMS over spp samples, (W, H, 3) [x][y]."""
         W, H = self.img_w, self.img_h
-        frame = np.zeros((W, H, 3), np.float32)
         devices = tuple(devices)
-        results = {}
-        errors = []
-
-        def run(rank, dev):
-            try:
-                ds = self.world.device_scene(dev)
-                ids = interleaved_tiles(W, H, tile, rank, len(devices))
-                sums, _ = ds.render_tiles(cam_packed, W, H, tile, tile, ids, spp, self.depth, seed, flags)
-                results[rank] = (ids, sums)
-            except Exception as e:  # surfaced below
-                errors.append(e)
-
-        if len(devices) == 1:
-            run(0, devices[0])
-        else:
-            for d in devices:
-                self.world.device_scene(d)
-            threads = [threading.Thread(target=run, args=(r, d)) for r, d in enumerate(devices)]
-            for t in threads:
-                t.start()
-            for t in threads:
-                t.join()
-        if errors:
-            raise errors[0]
-        for rank in sorted(results):
-            ids, sums = results[rank]
-            unpack_tiles(sums, W, H, tile, tile, ids, frame)
-        return frame
+        if len(devices) > 1:
+            return render_multi([self.world.device_scene(d) for d in devices], cam_packed, W, H, tile, spp,
+                                self.depth, seed, flags)
+        ds = self.world.device_scene(devices[0])
+        ids = interleaved_tiles(W, H, tile)
+        sums, _ = ds.render_tiles(cam_packed, W, H, tile, tile, ids, spp, self.depth, seed, flags)
+        return unpack_tiles(sums, W, H, tile, tile, ids)
 
     def render(self, cam_packed, spp, seed=0, devices=(0,), tile=64):
         if spp <= 0:

@@ -4,13 +4,17 @@
 // per-call workspaces (chunked per-sample radiance buffer, work counter), and
 // the launch sequence: memset(counter) -> trace_kernel -> reduce_kernel per
 // sample chunk, all on one stream.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -127,6 +131,10 @@ struct Scene {
     int ev_used = 0;
     size_t chunk_bytes = (size_t)4 << 30;  // per-sample buffer budget (HBM is 288 GB)
     size_t device_bytes = 0;
+    // prt_render / prt_render_multi (as the root): [x][y] output frame, gathered tile sums
+    // of every rank and their tile origins (host copy kept alive for the async upload)
+    DevBuf frame, gather, gather_xy;
+    std::vector<uint32_t> gather_xy_host;
 };
 
 struct DeviceGuard {
@@ -146,7 +154,8 @@ void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
     for (DevBuf* b : {&s->nodes4q, &s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v,
-                      &s->light_off, &s->sph, &s->sph_mat, &s->work, &s->stats})
+                      &s->light_off, &s->sph, &s->sph_mat, &s->work, &s->stats, &s->frame, &s->gather,
+                      &s->gather_xy})
         b->release();
     if (!s->ctx.empty()) (void)hipDeviceSynchronize();
     for (auto& c : s->ctx)
@@ -398,6 +407,76 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
                                    stream));
     }
     return PRT_OK;
+}
+
+// ---------------------------------------------------------------- RCCL ----
+// prt_render_multi's gather runs over RCCL.  librccl is resolved at first use with dlopen
+// (by SONAME first, so a process that already loaded torch's RCCL shares that instance
+// and its HIP runtime), which keeps libprt loadable on machines without RCCL: only
+// prt_render_multi then fails, with PRT_ERR_RCCL.
+struct Rccl {
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+    bool ok = false;
+    std::string why;
+};
+
+std::mutex g_comm_mu;   // guards g_rccl and g_comms
+Rccl g_rccl;
+bool g_rccl_tried = false;
+std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;   // per device list (root first)
+
+const Rccl& rccl() {
+    if (g_rccl_tried) return g_rccl;
+    g_rccl_tried = true;
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+        if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+    if (!h) {
+        g_rccl.why = std::string("librccl.so.1 not loadable: ") + (dlerror() ? dlerror() : "?");
+        return g_rccl;
+    }
+    auto sym = [&](const char* n) { return dlsym(h, n); };
+    g_rccl.comm_init_all = (decltype(g_rccl.comm_init_all))sym("ncclCommInitAll");
+    g_rccl.comm_destroy = (decltype(g_rccl.comm_destroy))sym("ncclCommDestroy");
+    g_rccl.group_start = (decltype(g_rccl.group_start))sym("ncclGroupStart");
+    g_rccl.group_end = (decltype(g_rccl.group_end))sym("ncclGroupEnd");
+    g_rccl.send = (decltype(g_rccl.send))sym("ncclSend");
+    g_rccl.recv = (decltype(g_rccl.recv))sym("ncclRecv");
+    g_rccl.error_string = (decltype(g_rccl.error_string))sym("ncclGetErrorString");
+    g_rccl.ok = g_rccl.comm_init_all && g_rccl.comm_destroy && g_rccl.group_start && g_rccl.group_end &&
+                g_rccl.send && g_rccl.recv && g_rccl.error_string;
+    if (!g_rccl.ok) g_rccl.why = "librccl lacks ncclCommInitAll / ncclSend / ncclRecv / group calls";
+    return g_rccl;
+}
+
+#define RCCL_TRY(expr)                                                                           \
+    do {                                                                                         \
+        ncclResult_t r_ = (expr);                                                                \
+        if (r_ != ncclSuccess) return fail(PRT_ERR_RCCL, std::string(#expr) + ": " + R.error_string(r_)); \
+    } while (0)
+
+// 'latin' tile owner of device_scene.tile_owner: rank = (tx + s * ty) mod n with s the
+// integer nearest 0.38 n that is coprime with n (every rank owns tiles in every row)
+int latin_stride(int n) {
+    int s = std::max(1, (int)std::lround(0.38 * n));
+    auto gcd = [](int a, int b) { while (b) { int t = a % b; a = b; b = t; } return a; };
+    while (gcd(s, n) != 1) ++s;
+    return s;
+}
+
+// tile ids of a window, ascending (tiles of tw x th in the W-wide frame)
+std::vector<int32_t> window_tiles(int W, int x0, int y0, int w, int h, int tw, int th) {
+    const int tiles_x = (W + tw - 1) / tw;
+    std::vector<int32_t> ids;
+    for (int ty = y0 / th; ty <= (y0 + h - 1) / th; ++ty)
+        for (int tx = x0 / tw; tx <= (x0 + w - 1) / tw; ++tx) ids.push_back(ty * tiles_x + tx);
+    return ids;
 }
 
 }  // namespace
@@ -744,6 +823,156 @@ int prt_diag_stats(void* scene, uint64_t* stats16) {
     HIP_TRY(hipMemcpy(h, s->stats.p, sizeof(h), hipMemcpyDeviceToHost));
     for (int i = 0; i < kStatWords; ++i) stats16[i] = h[i];
     return PRT_OK;
+}
+
+int prt_render(void* scene, const float* cam, int W, int H, int x0, int y0, int w, int h, int spp, int depth,
+               uint64_t seed, uint32_t flags, float* out_sum, uint64_t* stats) {
+    auto* s = (Scene*)scene;
+    if (!s) return fail(PRT_ERR_ARG, "scene is NULL");
+    if (w < 1 || h < 1 || x0 < 0 || y0 < 0 || (int64_t)x0 + w > W || (int64_t)y0 + h > H)
+        return fail(PRT_ERR_ARG, "window [x0, x0+w) x [y0, y0+h) must be non-empty and inside the W x H frame");
+    if (!out_sum) return fail(PRT_ERR_ARG, "out_sum is NULL");
+    // 8 x 8 tiles: one wave's 64 work items cover one square tile (coherent rays), and a
+    // window wastes at most a 7-pixel border of its edge tiles
+    constexpr int kT = 8;
+    std::vector<int32_t> ids = window_tiles(W, x0, y0, w, h, kT, kT);
+    int rc = check_render_args(s, cam, W, H, kT, kT, ids.data(), (int)ids.size(), spp, depth);
+    if (rc) return rc;
+    DeviceGuard g(s->device);
+    const int64_t n_slots = (int64_t)ids.size() * kT * kT;
+    RenderCtx* cx = ctx_for(s, s->stream);
+    if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
+    HIP_TRY(cx->acc.ensure(sizeof(float) * 3 * (size_t)n_slots));
+    const size_t out_bytes = sizeof(float) * 3 * (size_t)w * (size_t)h;
+    HIP_TRY(s->frame.ensure(out_bytes));
+    if ((rc = enqueue_render(s, cx, cam, W, H, kT, kT, ids.data(), (int)ids.size(), spp, depth, seed, flags,
+                             (float*)cx->acc.p)))
+        return rc;
+    HIP_TRY(prt::launch_scatter((const float*)cx->acc.p, (const uint32_t*)cx->tiles.p, (int)n_slots, 3, 6, x0, y0, w,
+                                h, (float*)s->frame.p, s->stream));
+    HIP_TRY(hipMemcpyAsync(out_sum, s->frame.p, out_bytes, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (read_fault_at(cx->work) != 0)
+        return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
+    if (stats) {
+        std::memset(stats, 0, 4 * sizeof(uint64_t));
+        if (flags & PRT_FLAG_STATS) {
+            unsigned long long hs[4];
+            HIP_TRY(hipMemcpy(hs, s->stats.p, sizeof(hs), hipMemcpyDeviceToHost));
+            for (int i = 0; i < 4; ++i) stats[i] = hs[i];
+        }
+    }
+    return PRT_OK;
+}
+
+int prt_render_multi(void* const* scenes, int n_scenes, const float* cam, int W, int H, int tile, int spp, int depth,
+                     uint64_t seed, uint32_t flags, float* out_frame) {
+    if (!scenes || n_scenes < 1) return fail(PRT_ERR_ARG, "need at least one scene handle");
+    if (!out_frame) return fail(PRT_ERR_ARG, "out_frame is NULL");
+    std::vector<Scene*> sc((size_t)n_scenes);
+    std::vector<int> devs((size_t)n_scenes);
+    for (int r = 0; r < n_scenes; ++r) {
+        sc[(size_t)r] = (Scene*)scenes[r];
+        if (!sc[(size_t)r]) return fail(PRT_ERR_ARG, "scene handle " + std::to_string(r) + " is NULL");
+        devs[(size_t)r] = sc[(size_t)r]->device;
+        for (int q = 0; q < r; ++q)
+            if (devs[(size_t)q] == devs[(size_t)r])
+                return fail(PRT_ERR_ARG, "scene handles must live on distinct devices (device " +
+                                             std::to_string(devs[(size_t)r]) + " twice)");
+    }
+    // tile ownership: the 'latin' interleave of device_scene.tile_owner
+    const int tiles_x = (W + tile - 1) / std::max(tile, 1), tiles_y = (H + tile - 1) / std::max(tile, 1);
+    const int stride = latin_stride(n_scenes);
+    std::vector<std::vector<int32_t>> ids((size_t)n_scenes);
+    for (int id = 0; id < tiles_x * tiles_y; ++id)
+        ids[(size_t)((id % tiles_x + (int64_t)stride * (id / tiles_x)) % n_scenes)].push_back(id);
+    for (int r = 0; r < n_scenes; ++r) {
+        int rc = check_render_args(sc[(size_t)r], cam, W, H, tile, tile, ids[(size_t)r].data(),
+                                   (int)ids[(size_t)r].size(), spp, depth);
+        if (rc) return rc;
+    }
+    std::lock_guard<std::mutex> lock(g_comm_mu);
+    const Rccl& R = rccl();
+    if (!R.ok) return fail(PRT_ERR_RCCL, R.why);
+    auto it = g_comms.find(devs);
+    if (it == g_comms.end()) {
+        std::vector<ncclComm_t> comms((size_t)n_scenes, nullptr);
+        RCCL_TRY(R.comm_init_all(comms.data(), n_scenes, devs.data()));
+        it = g_comms.emplace(devs, std::move(comms)).first;
+    }
+    const std::vector<ncclComm_t>& comms = it->second;
+    const int64_t slots = (int64_t)tile * tile;
+    const int log_t = __builtin_ctz((unsigned)tile);
+    // 1. every rank renders its tiles into its render context's sums (async, own stream)
+    std::vector<RenderCtx*> cx((size_t)n_scenes, nullptr);
+    std::vector<int64_t> off((size_t)n_scenes + 1, 0);
+    for (int r = 0; r < n_scenes; ++r) {
+        Scene* s = sc[(size_t)r];
+        DeviceGuard g(s->device);
+        const int nt = (int)ids[(size_t)r].size();
+        off[(size_t)r + 1] = off[(size_t)r] + nt * slots;
+        cx[(size_t)r] = ctx_for(s, s->stream);
+        if (!cx[(size_t)r]) return fail(PRT_ERR_OOM, "render context allocation failed");
+        HIP_TRY(cx[(size_t)r]->acc.ensure(std::max<size_t>(16, sizeof(float) * 3 * (size_t)(nt * slots))));
+        int rc = enqueue_render(s, cx[(size_t)r], cam, W, H, tile, tile, ids[(size_t)r].data(), nt, spp, depth, seed,
+                                flags, (float*)cx[(size_t)r]->acc.p);
+        if (rc) return rc;
+    }
+    // 2. root buffers: gathered sums of every rank (rank-major) and their tile origins
+    Scene* root = sc[0];
+    {
+        DeviceGuard g(root->device);
+        root->gather_xy_host.clear();
+        for (int r = 0; r < n_scenes; ++r)
+            for (int32_t id : ids[(size_t)r])
+                root->gather_xy_host.push_back(((uint32_t)((id % tiles_x) * tile) << 16) |
+                                               (uint32_t)((id / tiles_x) * tile));
+        HIP_TRY(root->gather.ensure(sizeof(float) * 3 * (size_t)off[(size_t)n_scenes]));
+        HIP_TRY(root->gather_xy.ensure(sizeof(uint32_t) * root->gather_xy_host.size()));
+        HIP_TRY(root->frame.ensure(sizeof(float) * 3 * (size_t)W * (size_t)H));
+        HIP_TRY(hipMemcpyAsync(root->gather_xy.p, root->gather_xy_host.data(),
+                               sizeof(uint32_t) * root->gather_xy_host.size(), hipMemcpyHostToDevice, root->stream));
+    }
+    // 3. the only exchange: every rank (the root too, through its self-loop) sends its packed
+    //    tile sums to the root in one RCCL group (point-to-point over xGMI; RCCL has no gather)
+    RCCL_TRY(R.group_start());
+    for (int r = 0; r < n_scenes; ++r) {
+        const size_t n = (size_t)(off[(size_t)r + 1] - off[(size_t)r]) * 3;
+        if (n == 0) continue;
+        Scene* s = sc[(size_t)r];
+        ncclResult_t e = R.send(cx[(size_t)r]->acc.p, n, ncclFloat32, 0, comms[(size_t)r], s->stream);
+        if (e == ncclSuccess)
+            e = R.recv((float*)root->gather.p + 3 * off[(size_t)r], n, ncclFloat32, r, comms[0], root->stream);
+        if (e != ncclSuccess) {
+            (void)R.group_end();
+            return fail(PRT_ERR_RCCL, std::string("ncclSend/ncclRecv: ") + R.error_string(e));
+        }
+    }
+    RCCL_TRY(R.group_end());
+    // 4. root: tiles -> [x][y] frame, frame -> host
+    {
+        DeviceGuard g(root->device);
+        HIP_TRY(prt::launch_scatter((const float*)root->gather.p, (const uint32_t*)root->gather_xy.p,
+                                    (int)off[(size_t)n_scenes], log_t, 2 * log_t, 0, 0, W, H, (float*)root->frame.p,
+                                    root->stream));
+        HIP_TRY(hipMemcpyAsync(out_frame, root->frame.p, sizeof(float) * 3 * (size_t)W * (size_t)H,
+                               hipMemcpyDeviceToHost, root->stream));
+    }
+    for (int r = 0; r < n_scenes; ++r) {
+        DeviceGuard g(sc[(size_t)r]->device);
+        HIP_TRY(hipStreamSynchronize(sc[(size_t)r]->stream));
+        if (read_fault_at(cx[(size_t)r]->work) != 0)
+            return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped on device " + std::to_string(devs[(size_t)r]));
+    }
+    return PRT_OK;
+}
+
+void prt_comm_release(void) {
+    std::lock_guard<std::mutex> lock(g_comm_mu);
+    if (g_rccl.ok)
+        for (auto& kv : g_comms)
+            for (ncclComm_t c : kv.second) (void)g_rccl.comm_destroy(c);
+    g_comms.clear();
 }
 
 }  // extern "C"

@@ -94,6 +94,9 @@ hipError_t launch_hits(const TraceParams& P, bool quantized, bool any, int stack
 size_t lds_scene_bytes(const TraceParams& P);  // LDS-resident scene + shading data
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);
+// packed tile slots (tile origins tile_xy) -> [x][y] window of the frame (prt_render, prt_render_multi)
+hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_slots, int log_tw, int log_tpx, int x0,
+                          int y0, int w, int h, float* out, hipStream_t stream);
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 
 }  // namespace prt

@@ -84,6 +84,27 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float
     hit_t[i] = hit ? ht : 0.0f;
 }
 
+// Packed tile slots -> a window [x0, x0+w) x [y0, y0+h) of the frame, indexed [x][y]
+// like the reference's pixels.to_numpy() (main_taichi.py:25): out[((x-x0)*h + (y-y0))*3 + c].
+// tile_xy = (x0 << 16) | y0 per tile (the trace kernel's tile origins); slots outside the
+// window (ragged frame edges, tiles straddling the window) are dropped.  Used by
+// prt_render (one window) and prt_render_multi (each rank's gathered tiles into the frame).
+__global__ __launch_bounds__(kBlock) void scatter_kernel(const float* __restrict__ packed,
+                                                         const uint32_t* __restrict__ tile_xy, int n_slots,
+                                                         int log_tw, int log_tpx, int x0, int y0, int w, int h,
+                                                         float* __restrict__ out) {
+    int slot = blockIdx.x * kBlock + threadIdx.x;
+    if (slot >= n_slots) return;
+    uint32_t xy = tile_xy[slot >> log_tpx];
+    int r = slot & ((1 << log_tpx) - 1);
+    int x = (int)(xy >> 16) + (r & ((1 << log_tw) - 1)) - x0;
+    int y = (int)(xy & 0xFFFFu) + (r >> log_tw) - y0;
+    if (x < 0 || y < 0 || x >= w || y >= h) return;
+    const float* p = packed + 3 * (size_t)slot;
+    float* o = out + ((size_t)x * h + y) * 3;
+    o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+}
+
 // Sequential per-pixel sum over this chunk's samples, in sample order, onto
 // the running sums (bit-identical to acc = acc + L[s] for s = 0..spp-1).
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict__ buf, float* __restrict__ acc,
@@ -150,6 +171,14 @@ hipError_t launch_hits(const TraceParams& P, bool quantized, bool any, int stack
         if (any) hits_kernel<false, true><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
         else hits_kernel<false, false><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_slots, int log_tw, int log_tpx, int x0,
+                          int y0, int w, int h, float* out, hipStream_t stream) {
+    if (n_slots <= 0) return hipSuccess;
+    scatter_kernel<<<(n_slots + kBlock - 1) / kBlock, kBlock, 0, stream>>>(packed, tile_xy, n_slots, log_tw, log_tpx,
+                                                                           x0, y0, w, h, out);
     return hipGetLastError();
 }
 

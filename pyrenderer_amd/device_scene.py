@@ -103,6 +103,16 @@ class DeviceScene:
                                          depth, int(seed), flags, N.ptr(out), N.ptr(stats)))
         return out, stats
 
+    def render_window(self, cam, W, H, x0, y0, w, h, spp, depth, seed=0, flags=0):
+        """prt_render: radiance sums of the window [x0, x0+w) x [y0, y0+h) of a W x H frame,
+        (w, h, 3) float32 indexed [x - x0][y - y0]; returns (sums, stats)."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        out = np.zeros((w, h, 3), np.float32)
+        stats = np.zeros(4, np.uint64)
+        N.check(N.lib().prt_render(self.h, N.ptr(cam), W, H, x0, y0, w, h, spp, depth, int(seed), flags, N.ptr(out),
+                                   N.ptr(stats)))
+        return out, stats
+
     def render_tiles_accumulate(self, cam, W, H, tw, th, tile_ids, first_sample, spp, depth, sums, seed=0, flags=0):
         """Progressive rendering: add samples first_sample .. first_sample+spp-1 onto `sums`
         ((n_tiles*tw*th, 3) float32, modified in place, slot order of render_tiles)."""
@@ -163,3 +173,15 @@ class DeviceScene:
         s = np.zeros(16, np.uint64)
         N.check(N.lib().prt_diag_stats(self.h, N.ptr(s)))
         return s
+
+
+def render_multi(scenes, cam, W, H, tile, spp, depth, seed=0, flags=0):
+    """prt_render_multi: the full frame's radiance sums (W, H, 3) [x][y] rendered over the
+    devices of `scenes` (DeviceScene handles on distinct GPUs of this process, scenes[0] the
+    root), gathered to the root with one RCCL send/recv group."""
+    cam = np.ascontiguousarray(cam, np.float32)
+    hs = (ctypes.c_void_p * len(scenes))(*[s.h for s in scenes])
+    out = np.zeros((W, H, 3), np.float32)
+    N.check(N.lib().prt_render_multi(hs, len(scenes), N.ptr(cam), W, H, tile, spp, depth, int(seed), flags,
+                                     N.ptr(out)))
+    return out

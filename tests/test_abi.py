@@ -120,3 +120,21 @@ def test_bvh_degenerate_inputs():
     assert sorted(same.export()[2].tolist()) == list(range(50))
     with pytest.raises(N.PrtError):
         N.Bvh(np.full((1, 9), np.nan, np.float32))
+
+
+def test_window_and_multi_argument_errors_without_gpu():
+    """prt_render / prt_render_multi reject bad handles and shapes before touching a device."""
+    import ctypes
+    from pyrenderer_amd import _native as N
+    L = N.lib()
+    cam = np.zeros(24, np.float32)
+    out = np.zeros((4, 4, 3), np.float32)
+    assert L.prt_render(None, N.ptr(cam), 4, 4, 0, 0, 4, 4, 1, 1, 0, 0, N.ptr(out), None) == -1
+    assert b"NULL" in L.prt_last_error()
+    assert L.prt_render_multi(None, 1, N.ptr(cam), 4, 4, 8, 1, 1, 0, 0, N.ptr(out)) == -1
+    hs = (ctypes.c_void_p * 2)(None, None)
+    assert L.prt_render_multi(hs, 0, N.ptr(cam), 4, 4, 8, 1, 1, 0, 0, N.ptr(out)) == -1
+    assert L.prt_render_multi(hs, 2, N.ptr(cam), 4, 4, 8, 1, 1, 0, 0, N.ptr(out)) == -1
+    assert b"NULL" in L.prt_last_error()
+    L.prt_comm_release()   # no communicator yet: a no-op
+
