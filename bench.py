@@ -17,7 +17,10 @@ streams when a rank renders < 8 M samples per frame, else serial frames).
 Rank 0 prints ONE JSON line with `roofline` (trace kernel, HBM-bound
 accounting: algorithmic bytes per launch from the counted traversal work ÷ the
 kernel's average duration measured with HIP events on its stream) and
-`cpu_baseline` (the oracle port, timed on this host on a bounded sample).
+`cpu_baseline` (the C oracle port with OpenMP, timed on this host on a bounded
+sample), plus `cpu_numpy` (N = 1): the NumPy restatement of main.py's path,
+one spawned process per core, on its own bounded sample, with its per-pixel
+comparison against the GPU frame.
 """
 import argparse
 import json
@@ -83,6 +86,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
+    ap.add_argument("--numpy-seconds", type=float, default=8.0,
+                    help="target wall time of the NumPy-path CPU sample (main.py counterpart); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc.json"),
                     help="PMC summaries per workload (tools/pmc_summary.py): HBM bytes per trace launch, "
@@ -144,6 +149,26 @@ def cpu_baseline(ids, dt, cores, args):
             "sample": f"{n} random 8x8 tiles of the {W}x{H} frame at {args.spp} spp, depth {args.depth} "
                       f"({samples} samples, {dt:.1f} s); oracle/prt_oracle.c (C port of PathTracer.trace), "
                       f"BVH2 closest hit, OpenMP {cores} threads"}
+
+
+def numpy_baseline(flat, cam, args, seconds):
+    """main.py's NumPy path counterpart (oracle/numpy_path.py: PathTracer.trace as array code
+    over ray batches, bit-identical to the C oracle), one spawned process per core like
+    main.py's joblib workers, on random 8x8 tiles sized to ~`seconds`.  Returns (report,
+    tile ids, sums) or (note, None, None) for scenes outside its scope (config 3, 4)."""
+    from oracle import numpy_path as NP
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    W = H = args.res
+    try:
+        ids, sums, dt = NP.timed_sample(flat, cam, W, H, args.spp, args.depth, args.seed, seconds, cores)
+    except NotImplementedError as e:
+        return {"value": None, "note": str(e)}, None, None
+    samples = len(ids) * 64 * args.spp
+    return ({"value": round(samples / dt / 1e6, 5), "unit": "Msamples/s", "cores": cores, "kind": "port",
+             "sample": f"{len(ids)} random 8x8 tiles of the {W}x{H} frame at {args.spp} spp, depth {args.depth} "
+                       f"({samples} samples, {dt:.1f} s); oracle/numpy_path.py (NumPy restatement of "
+                       f"PathTracer.trace over ray batches, brute-force closest hit), {cores} spawned processes"},
+            ids, sums)
 
 
 def l2_vs_cpu(gpu_sums, ids, cpu_sums, args):
@@ -270,7 +295,13 @@ def main():
             except (OSError, ValueError):
                 pmc = {}
             traffic = pmc.get("hbm_bytes_per_launch")
-        cpu, l2 = None, None
+        cpu, l2, cpu_np = None, None, None
+        if not args.no_cpu_baseline and world == 1 and args.numpy_seconds > 0:
+            cpu_np, np_ids, np_sums = numpy_baseline(flat, cam, args, args.numpy_seconds)
+            if np_ids is not None:
+                torch.cuda.synchronize(dev)
+                cmp = l2_vs_cpu(shards[0].assemble(), np_ids, np_sums, args)
+                cpu_np["l2_vs_gpu"] = {k: cmp[k] for k in ("pixels", "rmse", "max_pixel_l2", "identical_pixels")}
         if not args.no_cpu_baseline:
             # at N = 1 the baseline sample (~cpu_seconds) doubles as the accuracy sample; at
             # N > 1 only a short accuracy sample of the gathered frame is rendered on the CPU
@@ -308,6 +339,7 @@ def main():
                                 "ext_queries": round(ext / samples_per_step, 3),
                                 "shadow_queries": round(shadow / samples_per_step, 3)},
             "cpu_baseline": cpu,
+            "cpu_numpy": cpu_np,
             "l2_vs_cpu": l2,
         }
         print(json.dumps(line), flush=True)
