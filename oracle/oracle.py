@@ -73,6 +73,16 @@ def lib():
         L.or_closest_batch.argtypes = [_vp, _i, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         L.or_trace_scripted.argtypes = [_vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp]
         L.or_render_tiles.argtypes = [_vp, _i, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _i, _vp, _vp]
+        L.or_set_nee_mode.argtypes = [_i]
+        L.or_mis_power.argtypes = [_f, _f]
+        L.or_mis_power.restype = _f
+        L.or_area_light_pdf.argtypes = [_f, _vp, _vp]
+        L.or_area_light_pdf.restype = _f
+        L.or_brdf_pdf.argtypes = [_vp, _vp]
+        L.or_brdf_pdf.restype = _f
+        L.or_dot_or_zero.argtypes = [_vp, _vp]
+        L.or_dot_or_zero.restype = _f
+        L.or_direct_mis_scripted.argtypes = [_vp, _vp, _vp, _vp, _vp, _i, _vp]
         _lib = L
     return _lib
 
@@ -162,6 +172,14 @@ class OracleScene:
         lib().or_sample_light_scripted(self.h, _p(d), _p(p2), _p(n2), _p(e))
         return p2, n2, e
 
+    def direct_mis_scripted(self, p, n, rho, stream):
+        """sample_direct_lighting2 on a scripted stream: (direct radiance, draws consumed)."""
+        stream = _f32(stream)
+        out = np.zeros(3, np.float32)
+        used = lib().or_direct_mis_scripted(self.h, _p(_f32(p)), _p(_f32(n)), _p(_f32(rho)), _p(stream),
+                                            stream.shape[0], _p(out))
+        return out, used
+
     def trace_scripted(self, cam, W, H, x, y, depth, stream):
         stream = _f32(stream)
         out = np.zeros(3, np.float32)
@@ -202,6 +220,28 @@ def unpack_tiles(slots, W, H, tw, th, tile_ids):
         h = min(th, H - y0)
         frame[x0:x0 + w, y0:y0 + h] = s[k, :h, :w].transpose(1, 0, 2)
     return frame
+
+
+def set_nee_mode(mis):
+    """False = sample_direct_lighting (the path the reference's trace runs); True = the
+    MIS variant sample_direct_lighting2 (core/tracing.py:57-90) in its place."""
+    lib().or_set_nee_mode(1 if mis else 0)
+
+
+def mis_power(pf, pg):
+    return lib().or_mis_power(float(pf), float(pg))
+
+
+def area_light_pdf(t, d, n2):
+    return lib().or_area_light_pdf(float(t), _p(_f32(d)), _p(_f32(n2)))
+
+
+def brdf_pdf(n, d):
+    return lib().or_brdf_pdf(_p(_f32(n)), _p(_f32(d)))
+
+
+def dot_or_zero(n, d):
+    return lib().or_dot_or_zero(_p(_f32(n)), _p(_f32(d)))
 
 
 def set_trig_mode(mode):

@@ -700,6 +700,76 @@ static inline void sample_light(const OScene* s, Rng* rng, v3* p2, v3* n2, v3* e
     *e = mk(m[0], m[1], m[2]);  /* BSDFLight.evaluate() = (rho, rho, rho) */
 }
 
+/* ------------------------------------------- MIS direct lighting (variant) */
+/* The reference's unused helpers (core/tracing.py:12-39) and sample_direct_lighting2
+ * (core/tracing.py:57-90): one light-sampling and one BRDF-sampling strategy combined
+ * with the power heuristic, both visibility tests closest-hit queries over (1e-5,
+ * 9999.9) that must land on an emitter, light_area fixed at 1.0 (as the reference
+ * passes it), and the BRDF strategy's light pdf taken with the normal n2 of the
+ * LIGHT-SAMPLED point (the reference's quirk, kept).  trace() calls it instead of
+ * sample_direct_lighting when g_nee_mis is set (or_set_nee_mode). */
+static int g_nee_mis = 0;
+static const float kPiF = 3.14159265358979323846f;   /* np.pi in a Taichi f32 kernel */
+static const float kTMaxMis = 9999.9f;                /* core/tracing.py:67,80 */
+
+static inline float dot_or_zero(v3 n, v3 l) { float d = dot(n, l); return 0.0f > d ? 0.0f : d; }
+static inline float mis_power(float pf, float pg) {
+    float f = pf * pf, g = pg * pg;
+    return f / (f + g);
+}
+static inline float area_light_pdf(float t_light, v3 dir, v3 light_n, float light_area) {
+    float pdf = 0.0f;
+    float l_cos = dot(light_n, neg(dir));
+    if (l_cos > 1e-4f) {
+        v3 tmp = scl(dir, t_light);
+        float dist_sqr = dot(tmp, tmp);
+        pdf = dist_sqr / (light_area * l_cos);
+    }
+    return pdf;
+}
+static inline float brdf_pdf_of(v3 n, v3 dir) { return dot_or_zero(n, dir) / kPiF; }
+
+/* closest hit for the MIS queries; *emit = emitting_light of the hit primitive */
+static Hit mis_query(const OScene* s, int backend, v3 o, v3 d, Rng* rng, int scripted, uint64_t* cnt) {
+    if (cnt) cnt[3]++;
+    if (scripted) return hit_all_ref(s, o, d, kTMin, kTMaxMis, rng, 1, cnt);
+    return closest_hit(s, backend, o, d, kTMin, kTMaxMis, cnt);
+}
+
+static v3 direct_mis(const OScene* s, int backend, v3 p, v3 n, v3 rho, Rng* rng, int scripted, uint64_t* cnt) {
+    v3 p2, n2, e;
+    sample_light(s, rng, &p2, &n2, &e);
+    v3 direct = mk(0, 0, 0);
+    v3 fl = mul(scl(rho, kInvPi), e);   /* InvPi * hit_color * light_color */
+    v3 tl = normalize(sub(p2, p));
+    if (dot(tl, n) > 0.0f) {
+        Hit h = mis_query(s, backend, p, tl, rng, scripted, cnt);
+        if (h.hit && mat_of(s, h.tri)[3] > 0.0f) {
+            float lp = area_light_pdf(h.t, tl, n2, 1.0f);
+            float bp = brdf_pdf_of(n, tl);
+            if (lp > 0.0f && bp > 0.0f) {
+                float w = mis_power(lp, bp);
+                float nl = dot_or_zero(tl, n);
+                direct = add(direct, mk(fl.x * w * nl / lp, fl.y * w * nl / lp, fl.z * w * nl / lp));
+            }
+        }
+    }
+    v3 bd; float bp;
+    scatter(rng, n, &bd, &bp);   /* cosine_sample_hemisphere_convenient(hit_normal) */
+    if (bp > 0.0f) {
+        Hit h = mis_query(s, backend, p, bd, rng, scripted, cnt);
+        if (h.hit && mat_of(s, h.tri)[3] > 0.0f) {
+            float lp = area_light_pdf(h.t, bd, n2, 1.0f);
+            if (lp > 0.0f) {
+                float w = mis_power(bp, lp);
+                float nl = dot_or_zero(bd, n);
+                direct = add(direct, mk(fl.x * w * nl / bp, fl.y * w * nl / bp, fl.z * w * nl / bp));
+            }
+        }
+    }
+    return direct;
+}
+
 /* PathTracer.trace (core/tracing.py:116-155) + render() sample body. */
 static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, int H, int x, int y,
                        int depth, Rng* rng, int scripted, uint64_t* cnt) {
@@ -766,6 +836,12 @@ static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, in
             nb = mk(att.x * dz / pdf * kInvPi, att.y * dz / pdf * kInvPi, att.z * dz / pdf * kInvPi);
         }
         beta = mul(beta, nb);
+        if (g_nee_mis) {
+            /* variant: L += beta * sample_direct_lighting2(hit_pos, normal, attenuation) */
+            L = add(L, mul(beta, direct_mis(s, backend, p, n, att, rng, scripted, cnt)));
+            ro = p; rd = wi;
+            continue;
+        }
         /* sample_direct_lighting (tracing.py:92-108) */
         v3 p2, n2, e;
         sample_light(s, rng, &p2, &n2, &e);
@@ -842,6 +918,22 @@ OR_API void or_sample_light_scripted(void* p, const float* draws, float* p2, flo
     v3 a, b, c;
     sample_light(s, &r, &a, &b, &c);
     st3(p2, a); st3(n2, b); st3(e, c);
+}
+
+OR_API void or_set_nee_mode(int mis) { g_nee_mis = mis ? 1 : 0; }
+OR_API float or_mis_power(float pf, float pg) { return mis_power(pf, pg); }
+OR_API float or_area_light_pdf(float t, const float* d, const float* n2) { return area_light_pdf(t, ld3(d), ld3(n2), 1.0f); }
+OR_API float or_brdf_pdf(const float* n, const float* d) { return brdf_pdf_of(ld3(n), ld3(d)); }
+OR_API float or_dot_or_zero(const float* n, const float* d) { return dot_or_zero(ld3(n), ld3(d)); }
+/* sample_direct_lighting2 replayed on a scripted stream (reference order, hit_all's draws
+ * included); returns the number of draws consumed (-1 on stream overflow) */
+OR_API int or_direct_mis_scripted(void* p, const float* pos, const float* nrm, const float* rho, const float* stream,
+                                  int stream_len, float* out) {
+    OScene* s = (OScene*)p;
+    Rng r; memset(&r, 0, sizeof(r));
+    r.script = stream; r.script_len = stream_len;
+    st3(out, direct_mis(s, BACKEND_REF, ld3(pos), ld3(nrm), ld3(rho), &r, 1, NULL));
+    return r.overflow ? -1 : r.pos;
 }
 
 /* batch closest-hit: out_hit[i], out_t[i], out_tri[i], out_n[3i] */

@@ -32,6 +32,9 @@ Fixtures written (all under tests/golden/):
                       render() body of main_taichi.py:89-99 with SCRIPTED random
                       streams: per sample the stream, the pixel, the number of
                       draws consumed and the radiance returned.
+  mis_cornell.npz     PathTracer.sample_direct_lighting2 (core/tracing.py:57-90), the
+                      reference's unused MIS direct-lighting estimator, with scripted
+                      streams at camera-ray hit points, and its helpers' unit vectors.
   image_d{D}.npz      statistical reference image: per-pixel mean and standard
                       error of main_taichi.py's render() at res×res, spp, depth D.
 """
@@ -382,6 +385,58 @@ def gen_trace(n_samples=1500, depths=(4, 8), stream_len=256, res=512):
     np.savez_compressed(os.path.join(OUT, "trace_cornell.npz"), **out)
 
 
+def gen_mis(n=1500, stream_len=64, res=512):
+    """mis_cornell.npz: the reference's unused MIS direct-lighting estimator
+    PathTracer.sample_direct_lighting2 (core/tracing.py:57-90) at surface points hit by
+    camera rays, replayed with SCRIPTED random streams (inputs, stream, draws consumed,
+    result), plus unit vectors of its helpers mis_power_heuristic / compute_area_light_pdf
+    / compute_brdf_pdf / dot_or_zero (core/tracing.py:12-39)."""
+    ti, scene, cam, world = _load()
+    from core.tracing import (PathTracer, compute_area_light_pdf, compute_brdf_pdf, dot_or_zero,
+                              mis_power_heuristic)
+    tc = cam.convert_to_taichi_camera()
+    tracer = PathTracer(world, 8, res, res)
+    rng = np.random.default_rng(777)
+    pts, nrms, rhos, streams, outs, used = [], [], [], [], [], []
+    while len(pts) < n:
+        x, y = (int(v) for v in rng.integers(0, res, 2))
+        ti.script_random(rng.random(64).astype(np.float32))
+        u = (x + ti.random()) / (res - 1)
+        v = (y + ti.random()) / (res - 1)
+        o, d = tc.gen_ray(u, v)
+        hit, t, p, nrm, emissive, att, _, _ = world.hit_all(o, d, 0.00001, 99999.9)
+        ti.script_random(None)
+        if not hit or emissive > 0:
+            continue
+        st = rng.random(stream_len).astype(np.float32)
+        ti.script_random(st)
+        li = tracer.sample_direct_lighting2(p, nrm, att)
+        used.append(ti.script_consumed())
+        ti.script_random(None)
+        pts.append(np.asarray(p, np.float32)); nrms.append(np.asarray(nrm, np.float32))
+        rhos.append(np.asarray(att, np.float32)); streams.append(st); outs.append(np.asarray(li, np.float32))
+    out = dict(p=np.stack(pts), n=np.stack(nrms), rho=np.stack(rhos), streams=np.stack(streams),
+               direct=np.stack(outs), used=np.asarray(used, np.int32))
+    k = 400
+    pf = (rng.random(k) * 4).astype(np.float32)
+    pg = (rng.random(k) * 4).astype(np.float32)
+    out["pw_f"], out["pw_g"] = pf, pg
+    out["pw_out"] = np.array([mis_power_heuristic(pf[i], pg[i]) for i in range(k)], np.float32)
+    dirs = rng.normal(size=(k, 3)).astype(np.float32)
+    dirs = (dirs / np.linalg.norm(dirs, axis=1, keepdims=True)).astype(np.float32)
+    n2 = rng.normal(size=(k, 3)).astype(np.float32)
+    n2 = (n2 / np.linalg.norm(n2, axis=1, keepdims=True)).astype(np.float32)
+    tl = (rng.random(k) * 5).astype(np.float32)
+    out["ap_t"], out["ap_d"], out["ap_n"] = tl, dirs, n2
+    out["ap_out"] = np.array([compute_area_light_pdf(tl[i], ti.Vec(dirs[i]), ti.Vec(n2[i]), 1.0)
+                              for i in range(k)], np.float32)
+    out["bp_out"] = np.array([compute_brdf_pdf(ti.Vec(n2[i]), ti.Vec(dirs[i])) for i in range(k)], np.float32)
+    out["dz_out"] = np.array([dot_or_zero(ti.Vec(n2[i]), ti.Vec(dirs[i])) for i in range(k)], np.float32)
+    np.savez_compressed(os.path.join(OUT, "mis_cornell.npz"), **out)
+    nz = (np.abs(out["direct"]).sum(1) > 0).mean()
+    print(f"mis_cornell.npz: {n} points, non-zero direct {nz:.2f}, draws {np.mean(used):.1f}")
+
+
 def _image_worker(args):
     rows, res, spp, depth, seed = args
     ti, scene, cam, world = _load()
@@ -425,7 +480,7 @@ def gen_image(depth, res, spp, procs):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["scene", "hits", "kats", "trace", "image"])
+    ap.add_argument("what", nargs="+", choices=["scene", "hits", "kats", "trace", "mis", "image"])
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--res", type=int, default=32)
     ap.add_argument("--spp", type=int, default=256)
@@ -440,5 +495,7 @@ if __name__ == "__main__":
             gen_kats()
         elif w == "trace":
             gen_trace()
+        elif w == "mis":
+            gen_mis()
         elif w == "image":
             gen_image(a.depth, a.res, a.spp, a.procs)

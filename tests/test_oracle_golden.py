@@ -135,3 +135,26 @@ def test_trace_scripted_bit_exact(oracle_scene, cornell, depth):
         out, used = oracle_scene.trace_scripted(cam, res, res, x, y, depth, tr[f"d{depth}_streams"][i])
         assert used == tr[f"d{depth}_used"][i], i
         np.testing.assert_array_equal(out, tr[f"d{depth}_color"][i])
+
+
+def test_mis_helpers_kat():
+    """core/tracing.py:12-39: dot_or_zero, mis_power_heuristic, compute_area_light_pdf
+    (light_area 1.0), compute_brdf_pdf — vectors produced by the reference's code."""
+    k = golden("mis_cornell.npz")
+    for i in range(k["pw_f"].shape[0]):
+        assert O.mis_power(k["pw_f"][i], k["pw_g"][i]) == k["pw_out"][i], i
+        assert O.area_light_pdf(k["ap_t"][i], k["ap_d"][i], k["ap_n"][i]) == k["ap_out"][i], i
+        assert O.brdf_pdf(k["ap_n"][i], k["ap_d"][i]) == k["bp_out"][i], i
+        assert O.dot_or_zero(k["ap_n"][i], k["ap_d"][i]) == k["dz_out"][i], i
+
+
+def test_mis_direct_lighting_scripted(oracle_scene):
+    """PathTracer.sample_direct_lighting2 (core/tracing.py:57-90), the reference's unused
+    MIS estimator, replayed on the reference's own draws: result and draws consumed."""
+    O.set_trig_mode(1)
+    k = golden("mis_cornell.npz")
+    for i in range(k["p"].shape[0]):
+        out, used = oracle_scene.direct_mis_scripted(k["p"][i], k["n"][i], k["rho"][i], k["streams"][i])
+        assert used == k["used"][i], i
+        np.testing.assert_array_equal(out, k["direct"][i], err_msg=str(i))
+    O.set_trig_mode(0)
