@@ -42,6 +42,13 @@ extern "C" {
 #define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
 #define PRT_FLAG_TIME 0x2u   /* time the trace kernel with HIP events on its stream */
 #define PRT_FLAG_NO_PRIMARY_KERNEL 0x4u /* generate camera rays inside the trace kernel (A/B; same image) */
+/* estimator variant: direct lighting by the reference's unused MIS function
+ * PathTracer.sample_direct_lighting2 (core/tracing.py:57-90, helpers :12-39) in place of
+ * sample_direct_lighting — two closest-hit visibility queries per diffuse vertex (light
+ * and BRDF strategies, power heuristic, light_area 1.0 as the reference passes it).
+ * A different estimator: the image differs from the default one (oracle: or_set_nee_mode).
+ * Selects the MIS kernel variants (32, 33); an explicit variant must agree with the flag. */
+#define PRT_FLAG_MIS_NEE 0x8u
 /* trace-kernel variant in bits 8..15 (0 = automatic; the numbering is the
  * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: split / unified / while-while
  * traversal, BVH2 / BVH4, global / LDS-resident scene, occupancy targets,

@@ -14,8 +14,11 @@ PRT_OK = 0
 PRT_FLAG_STATS = 0x1
 PRT_FLAG_TIME = 0x2
 PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
-# trace-kernel variant ids 1..VAR_LAST (pyrenderer_amd/csrc/prt_kernels.h)
+PRT_FLAG_MIS_NEE = 0x8
+# trace-kernel variant ids 1..VAR_LAST of the reference estimator (pyrenderer_amd/csrc/prt_kernels.h);
+# the MIS direct-lighting estimator's variants (PRT_FLAG_MIS_NEE) follow
 VAR_LAST = 31
+VAR_MIS = (32, 33)
 VAR_WW4_PH_LDS6 = 15
 VAR_WW4_Q_SP5 = 23
 PRT_HITS_ANY = 0x1

@@ -47,10 +47,22 @@ class PathTracer:
         sums, _ = ds.render_tiles(cam_packed, W, H, tile, tile, ids, spp, self.depth, seed, flags)
         return unpack_tiles(sums, W, H, tile, tile, ids)
 
-    def render(self, cam_packed, spp, seed=0, devices=(0,), tile=64):
+    def render(self, cam_packed, spp, seed=0, devices=(0,), tile=64, nee="reference"):
         if spp <= 0:
             return np.zeros((self.img_w, self.img_h, 3), np.float32)
-        return self.render_sums(cam_packed, spp, seed, devices, tile) / np.float32(spp)
+        return self.render_sums(cam_packed, spp, seed, devices, tile, nee_flags(nee)) / np.float32(spp)
+
+
+def nee_flags(nee):
+    """Direct-lighting estimator: 'reference' = sample_direct_lighting, the one the
+    reference's trace calls (core/tracing.py:92-108, :150-151); 'mis' = its unused MIS
+    alternative sample_direct_lighting2 (core/tracing.py:57-90) in the same place."""
+    from .._native import PRT_FLAG_MIS_NEE
+    if nee == "reference":
+        return 0
+    if nee == "mis":
+        return PRT_FLAG_MIS_NEE
+    raise ValueError(f"nee must be 'reference' or 'mis', not {nee!r}")
 
 
 def build_world(scene, devices=(0,)):
@@ -60,8 +72,12 @@ def build_world(scene, devices=(0,)):
     return world.commit(devices)
 
 
-def render(scene, camera, *, spp, depth, seed=0, resolution=None, devices=(0,), tile=64, world=None):
+def render(scene, camera, *, spp, depth, seed=0, resolution=None, devices=(0,), tile=64, world=None,
+           nee="reference"):
     """Mean linear radiance (W, H, 3) float32, [x][y], y up.
+
+    nee: 'reference' (sample_direct_lighting, what the reference's trace runs) or 'mis'
+    (the reference's unused MIS estimator sample_direct_lighting2, as an optional variant).
 
     resolution: (W, H) override of camera.resolution (the aspect ratio still
     comes from camera.resolution, as convert_to_taichi_camera() does).
@@ -69,7 +85,7 @@ def render(scene, camera, *, spp, depth, seed=0, resolution=None, devices=(0,), 
     W, H = resolution if resolution is not None else camera.resolution
     world = world or build_world(scene, devices)
     tracer = PathTracer(world, depth, int(W), int(H))
-    return tracer.render(camera.convert_to_taichi_camera().packed(), spp, seed, devices, tile)
+    return tracer.render(camera.convert_to_taichi_camera().packed(), spp, seed, devices, tile, nee)
 
 
 class Accumulator:

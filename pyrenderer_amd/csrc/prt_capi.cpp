@@ -351,8 +351,12 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     P.sph = (const float4*)s->sph.p;
     P.sph_mat = (const int*)s->sph_mat.p;
     int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFFu);
-    if (var == 0) var = default_variant(s);
+    const bool mis = (flags & PRT_FLAG_MIS_NEE) != 0;
+    if (var == 0)
+        var = !mis ? default_variant(s) : (lds_fits4(s) && s->stack4) ? prt::kVarWW4Lds6Mis : prt::kVarWW4QRSp6Mis;
     if (var < prt::kVarSplit || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
+    if (prt::variant_mis(var) != mis)
+        return fail(PRT_ERR_ARG, "PRT_FLAG_MIS_NEE must be set exactly for the MIS estimator variants");
     const bool b4 = prt::variant_uses_bvh4(var);
     const bool spill = prt::variant_spills(var);
     if (b4) {

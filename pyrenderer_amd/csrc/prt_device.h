@@ -796,7 +796,29 @@ __device__ __forceinline__ void camera_ray(const TraceParams& P, int x, int y, u
     }
 }
 
-enum : int { Q_EXT = 0, Q_SHADOW = 1 };
+enum : int { Q_EXT = 0, Q_SHADOW = 1, Q_MISL = 2, Q_MISB = 3 };
+
+// MIS direct-lighting variant (VAR & 256): the reference's unused estimator
+// PathTracer.sample_direct_lighting2 and its helpers (core/tracing.py:12-90), restated
+// as oracle/prt_oracle.c:direct_mis.  Both strategies' visibility tests are closest-hit
+// queries over (1e-5, 9999.9) that must land on an emitter; light_area = 1.0 and the
+// BRDF strategy's light pdf uses the light-sampled point's normal, as the reference has it.
+constexpr float kTMaxMis = 9999.9f;
+constexpr float kPiF = 3.14159265358979323846f;   // np.pi inside a Taichi f32 kernel
+__device__ __forceinline__ float dot_or_zero(V3 n, V3 l) { float d = dot(n, l); return 0.0f > d ? 0.0f : d; }
+__device__ __forceinline__ float mis_power(float pf, float pg) {
+    float f = pf * pf, g = pg * pg;
+    return f / (f + g);
+}
+__device__ __forceinline__ float area_light_pdf(float t_light, V3 dir, V3 light_n) {
+    float pdf = 0.0f;
+    float l_cos = dot(light_n, neg(dir));
+    if (l_cos > 1e-4f) {
+        V3 tmp = dir * t_light;
+        pdf = dot(tmp, tmp) / (1.0f * l_cos);
+    }
+    return pdf;
+}
 
 template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
@@ -808,6 +830,7 @@ void trace_kernel(TraceParams P) {
     constexpr bool SPILL = (VAR & 32) != 0;    // LDS stack of STACK entries + global spill area
     constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
     constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
+    constexpr bool MIS = (VAR & 256) != 0;     // MIS direct lighting (sample_direct_lighting2) instead of NEE
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
     // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
@@ -869,6 +892,10 @@ void trace_kernel(TraceParams P) {
     uint32_t st = 0;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
     V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
+    // MIS: shading normal, light-sampled point's normal, InvPi * rho * light colour, the
+    // BRDF-strategy direction and pdf of the current vertex (pend accumulates direct_li)
+    V3 mis_n = v3(0, 0, 0), mis_n2 = v3(0, 0, 0), mis_fl = v3(0, 0, 0), mis_bd = v3(0, 0, 0);
+    float mis_bp = 0.0f;
     float tmax = kTMax;
     Counters cn = {0, 0, 0, 0, 0, 0, 0};
     uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
@@ -1119,8 +1146,8 @@ void trace_kernel(TraceParams P) {
                     float u0 = rng_next(st);
                     float u1 = rng_next(st);
                     V3 l = cosine_hemisphere(u0, u1);
+                    const float4* fr = s_fr + ((size_t)(hid < P.n_tri ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
                     if (hid < P.n_tri) {
-                        const float4* fr = s_fr + ((size_t)hid * 2 + (flip ? 1 : 0)) * 3;
                         float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
                         wi = normalize(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
                     } else {
@@ -1151,6 +1178,41 @@ void trace_kernel(TraceParams P) {
                     float c = 1.0f - a - b;
                     V3 p2 = (xyz(L0) * a + xyz(L1) * b) + xyz(L2) * c;
                     V3 n2 = xyz(LN);
+                    if constexpr (MIS) {
+                        // sample_direct_lighting2: the BRDF strategy's direction is drawn now
+                        // (queries draw nothing, so the stream order is the reference's)
+                        const float* em = s_mats + 8 * __float_as_int(LN.w);
+                        mis_fl = v3(m[0] * kInvPi * em[0], m[1] * kInvPi * em[1], m[2] * kInvPi * em[2]);
+                        V3 tl = normalize(p2 - p);
+                        float b0 = rng_next(st);
+                        float b1 = rng_next(st);
+                        V3 bl = cosine_hemisphere(b0, b1);
+                        if (hid < P.n_tri) {
+                            float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
+                            mis_bd = normalize(xyz(f0) * bl.x + xyz(f1) * bl.y + xyz(f2) * bl.z);
+                        } else {
+                            mis_bd = to_world(n, bl);
+                        }
+                        mis_bp = fabsf(dot(n, mis_bd)) * kInvPi;
+                        mis_n = n;
+                        mis_n2 = n2;
+                        pend = v3(0, 0, 0);
+                        o = p;
+                        tmax = kTMaxMis;
+                        if (dot(tl, n) > 0.0f) {
+                            d = tl;
+                            qtype = Q_MISL;
+                        } else if (mis_bp > 0.0f) {
+                            d = mis_bd;
+                            qtype = Q_MISB;
+                        } else {
+                            L = L + beta * pend;
+                            ++bounce;
+                            if (bounce >= P.depth) finished = true;
+                            d = wi;
+                            tmax = kTMax;
+                        }
+                    } else {
                     V3 w = normalize(p2 - p);
                     float t_at = (p2.x - p.x) / w.x;
                     // w2 = normalize(p - p2) is -w bit for bit (round-to-nearest is sign
@@ -1175,8 +1237,54 @@ void trace_kernel(TraceParams P) {
                         d = wi;
                         tmax = kTMax;
                     }
+                    }   // !MIS
                 }
             }
+        } else if (MIS && qtype == Q_MISL) {
+            // light strategy: visible when the closest hit is an emitter
+            if (hit) {
+                const int mid = hid < P.n_tri ? __float_as_int(s_nm[hid].w) : P.sph_mat[hid - P.n_tri];
+                if (s_mats[8 * mid + 3] > 0.0f) {
+                    float lp = area_light_pdf(ht, d, mis_n2);
+                    float bp = dot_or_zero(mis_n, d) / kPiF;
+                    if (lp > 0.0f && bp > 0.0f) {
+                        float w = mis_power(lp, bp);
+                        float nl = dot_or_zero(d, mis_n);
+                        pend = pend + v3(mis_fl.x * w * nl / lp, mis_fl.y * w * nl / lp, mis_fl.z * w * nl / lp);
+                    }
+                }
+            }
+            if (mis_bp > 0.0f) {
+                d = mis_bd;          // o is still the vertex, tmax kTMaxMis
+                qtype = Q_MISB;
+            } else {
+                L = L + beta * pend;
+                ++bounce;
+                if (bounce >= P.depth) finished = true;
+                d = wi;
+                tmax = kTMax;
+                qtype = Q_EXT;
+            }
+        } else if (MIS && qtype == Q_MISB) {
+            // BRDF strategy
+            if (hit) {
+                const int mid = hid < P.n_tri ? __float_as_int(s_nm[hid].w) : P.sph_mat[hid - P.n_tri];
+                if (s_mats[8 * mid + 3] > 0.0f) {
+                    float lp = area_light_pdf(ht, d, mis_n2);
+                    if (lp > 0.0f) {
+                        float w = mis_power(mis_bp, lp);
+                        float nl = dot_or_zero(d, mis_n);
+                        pend = pend + v3(mis_fl.x * w * nl / mis_bp, mis_fl.y * w * nl / mis_bp,
+                                         mis_fl.z * w * nl / mis_bp);
+                    }
+                }
+            }
+            L = L + beta * pend;
+            ++bounce;
+            if (bounce >= P.depth) finished = true;
+            d = wi;
+            tmax = kTMax;
+            qtype = Q_EXT;
         } else {
             if (!hit) L = L + pend;
             ++bounce;
@@ -1261,7 +1369,9 @@ void trace_kernel(TraceParams P) {
     X(kVarWW4QRSp5, 227, false, 5)                       \
     X(kVarWW4PhLds7, 11, true, 7)                        \
     X(kVarWW4PhLds5, 11, true, 5)                        \
-    X(kVarWW4QRSp6, 227, false, 6)
+    X(kVarWW4QRSp6, 227, false, 6)                       \
+    X(kVarWW4Lds6Mis, 259, true, 6)                      \
+    X(kVarWW4QRSp6Mis, 483, false, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>

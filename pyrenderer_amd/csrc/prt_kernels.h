@@ -80,7 +80,11 @@ constexpr int kVarWW4QRSp5 = 28;    // resume, quantised nodes, spill stack, >= 
 constexpr int kVarWW4PhLds7 = 29;   // phase-aligned, LDS scene, >= 7 waves per SIMD
 constexpr int kVarWW4PhLds5 = 30;   // ... >= 5 waves per SIMD
 constexpr int kVarWW4QRSp6 = 31;   // resume, quantised nodes, spill stack, >= 6 waves per SIMD
-constexpr int kVarLast = 31;
+// estimator variants: the reference's unused MIS direct lighting (PRT_FLAG_MIS_NEE)
+constexpr int kVarWW4Lds6Mis = 32;   // kVarWW4Lds6 + MIS, LDS scene
+constexpr int kVarWW4QRSp6Mis = 33;  // kVarWW4QRSp6 + MIS, global scene
+constexpr int kVarLast = 33;
+bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
 bool variant_quantized(int var);

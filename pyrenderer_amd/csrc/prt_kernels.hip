@@ -203,6 +203,15 @@ bool variant_uses_bvh4(int var) {
     }
 }
 
+bool variant_mis(int var) {
+    switch (var) {
+#define X(id, trav, lds, wpe) case id: return (trav & 256) != 0;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
 bool variant_quantized(int var) {
     switch (var) {
 #define X(id, trav, lds, wpe) case id: return (trav & 64) != 0;

@@ -300,3 +300,53 @@ def test_large_frame_matches_oracle(gpu_scene, oracle_scene, cornell):
     o = oracle_scene.render(cam, W, H, 32, 8, seed=0, nthreads=min(16, len(os.sched_getaffinity(0))))
     diff = np.any(g != o, axis=-1)
     assert not diff.any(), (int(diff.sum()), np.argwhere(diff)[:5])
+
+
+def test_mis_direct_lighting_variant_matches_oracle(gpu_scene, oracle_scene, cornell):
+    """The reference's unused MIS estimator (sample_direct_lighting2, core/tracing.py:57-90)
+    as the optional NEE variant: LDS-scene kernel (variant 32) bit-identical to the oracle's
+    MIS mode, and different from the default estimator's image."""
+    from pyrenderer_amd import _native as N
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    W, H, spp, depth = 64, 48, 4, 8
+    ids = np.arange(((W + 31) // 32) * ((H + 31) // 32), dtype=np.int32)
+    O.set_nee_mode(True)
+    try:
+        o = oracle_scene.render_tiles(cam, W, H, 32, 32, ids, spp, depth, seed=4)
+        oc = oracle_scene.render_tiles(cam, W, H, 32, 32, ids, 2, depth, seed=4, counters=True)[1]
+    finally:
+        O.set_nee_mode(False)
+    g, _ = gpu_scene.render_tiles(cam, W, H, 32, 32, ids, spp, depth, 4, N.PRT_FLAG_MIS_NEE)
+    assert np.isfinite(g).all() and g.any()
+    np.testing.assert_array_equal(g, o)
+    _, st = gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 2, depth, 4, N.PRT_FLAG_MIS_NEE | N.PRT_FLAG_STATS)
+    assert st[2] == oc[2] and st[3] == oc[3], (st, oc)
+    ref, _ = gpu_scene.render_tiles(cam, W, H, 32, 32, ids, spp, depth, 4)
+    assert not np.array_equal(g, ref)
+    # the global-scene MIS kernel (quantised BVH4, spill stack, resume) gives the same bits
+    g2, _ = gpu_scene.render_tiles(cam, W, H, 32, 32, ids, spp, depth, 4, N.PRT_FLAG_MIS_NEE | (N.VAR_MIS[1] << 8))
+    np.testing.assert_array_equal(g2, o)
+    # flag and variant must agree
+    with pytest.raises(N.PrtError):
+        gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, N.VAR_MIS[0] << 8)
+    with pytest.raises(N.PrtError):
+        gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, N.PRT_FLAG_MIS_NEE | (15 << 8))
+
+
+def test_mis_variant_on_a_global_scene_matches_oracle(cornell):
+    """MIS estimator on a scene too large for LDS (default global MIS kernel, variant 33)."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    flat = _soup_scene(cornell, 3000, 11)
+    ds = DeviceScene(flat, 0)
+    osc = O.OracleScene.from_flat(flat)
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    ids = np.arange(4, dtype=np.int32)
+    O.set_nee_mode(True)
+    try:
+        o = osc.render_tiles(cam, 64, 64, 32, 32, ids, 2, 8, seed=6)
+    finally:
+        O.set_nee_mode(False)
+    g, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 2, 8, 6, N.PRT_FLAG_MIS_NEE)
+    np.testing.assert_array_equal(g, o)
+    ds.close()
