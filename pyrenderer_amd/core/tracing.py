@@ -99,7 +99,8 @@ class Accumulator:
     count, seed, depth, resolution, tile).
     """
 
-    def __init__(self, scene, camera, *, depth, seed=0, resolution=None, device=0, tile=64, world=None):
+    def __init__(self, scene, camera, *, depth, seed=0, resolution=None, device=0, tile=64, world=None,
+                 nee="reference"):
         W, H = resolution if resolution is not None else camera.resolution
         self.W, self.H, self.depth, self.seed, self.tile = int(W), int(H), int(depth), int(seed), int(tile)
         self.device = device
@@ -108,6 +109,7 @@ class Accumulator:
         self.ids = interleaved_tiles(self.W, self.H, self.tile)
         self.slots = np.zeros((self.ids.shape[0] * self.tile * self.tile, 3), np.float32)
         self.samples = 0
+        self.flags = nee_flags(nee)
 
     def add(self, spp=1):
         """Render samples [samples, samples + spp) of every pixel onto the sums."""
@@ -115,7 +117,7 @@ class Accumulator:
             raise ValueError("spp must be >= 0")
         ds = self.world.device_scene(self.device)
         ds.render_tiles_accumulate(self.cam, self.W, self.H, self.tile, self.tile, self.ids, self.samples, spp,
-                                   self.depth, self.slots, self.seed)
+                                   self.depth, self.slots, self.seed, self.flags)
         self.samples += spp
         return self
 
@@ -131,7 +133,7 @@ class Accumulator:
     def state(self):
         return dict(slots=self.slots, samples=np.int64(self.samples), seed=np.int64(self.seed),
                     depth=np.int64(self.depth), resolution=np.array([self.W, self.H], np.int64),
-                    tile=np.int64(self.tile))
+                    tile=np.int64(self.tile), flags=np.int64(self.flags))
 
     def save(self, path):
         np.savez(path, **self.state())
@@ -140,8 +142,9 @@ class Accumulator:
     def load(cls, path, scene, camera, device=0, world=None):
         z = np.load(path, allow_pickle=False)
         W, H = (int(v) for v in z["resolution"])
+        mis = "flags" in z.files and int(z["flags"]) & nee_flags("mis")
         acc = cls(scene, camera, depth=int(z["depth"]), seed=int(z["seed"]), resolution=(W, H), device=device,
-                  tile=int(z["tile"]), world=world)
+                  tile=int(z["tile"]), world=world, nee="mis" if mis else "reference")
         if z["slots"].shape != acc.slots.shape:
             raise ValueError("saved accumulation does not match the frame layout")
         acc.slots[...] = z["slots"]

@@ -80,3 +80,23 @@ def test_tracing_render_all_devices(cornell, oracle_scene):
     mean = render(scene, camera, spp=2, depth=8, seed=9, resolution=(96, 64), devices=devs)
     cam = camera.convert_to_taichi_camera().packed()
     np.testing.assert_array_equal(mean, oracle_scene.render(cam, 96, 64, 2, 8, seed=9) / np.float32(2))
+
+
+def test_cli_progressive_resume_equals_one_render(tmp_path, cornell):
+    """python -m pyrenderer_amd (main_taichi.py's loop without the GUI): progressive passes
+    with a saved / resumed accumulation give the one-shot render's image bit for bit, and
+    the PNG is written."""
+    from pyrenderer_amd.core.tracing import render
+    from pyrenderer_amd.main import main
+    state = str(tmp_path / "acc.npz")
+    common = ["--resolution", "48", "32", "--depth", "8", "--seed", "3"]
+    main(common + ["--samples", "3", "--interval", "2", "--state", state, "--out", ""])
+    mean = main(common + ["--samples", "6", "--interval", "2", "--state", state,
+                          "--out", str(tmp_path / "o.png"), "--hdr", str(tmp_path / "o.npy")])
+    ref = render(cornell[0], cornell[1], spp=6, depth=8, seed=3, resolution=(48, 32))
+    np.testing.assert_array_equal(mean, ref)
+    np.testing.assert_array_equal(np.load(tmp_path / "o.npy"), ref)
+    assert (tmp_path / "o.png").read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"
+    m2 = main(common + ["--samples", "2", "--nee", "mis", "--out", "", "--tonemap", "reinhard"])
+    assert np.isfinite(m2).all() and not np.array_equal(m2, render(cornell[0], cornell[1], spp=2, depth=8, seed=3,
+                                                                     resolution=(48, 32)))

@@ -86,3 +86,12 @@ def test_obj_loader_and_tile_unpack():
     xs, ys = np.meshgrid(np.arange(100), np.arange(70), indexing="ij")
     np.testing.assert_array_equal(frame[..., 0], xs)
     np.testing.assert_array_equal(frame[..., 1], ys)
+
+
+def test_cli_arguments():
+    """The CLI's flags (python -m pyrenderer_amd): parsing only, no device work."""
+    from pyrenderer_amd.main import DEFAULT_SCENE, parse
+    a = parse([])
+    assert a.scene == DEFAULT_SCENE and a.samples == 64 and a.depth == 16 and a.devices == [0]
+    a = parse(["x.json", "--samples", "8", "--devices", "0", "1", "--nee", "mis", "--resolution", "64", "32"])
+    assert a.samples == 8 and a.devices == [0, 1] and a.nee == "mis" and a.resolution == [64, 32]
