@@ -245,11 +245,11 @@ def main():
     # counted traversal work of one frame (deterministic: same RNG as the timed steps)
     step(N.PRT_FLAG_STATS)
     torch.cuda.synchronize(dev)
-    st = ds.last_stats().astype(np.float64)
+    st = np.append(ds.last_stats().astype(np.float64), float(ds.diag_stats()[14]))
     cnt = torch.tensor(st, dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(cnt)
-    nodes, tris, ext, shadow = cnt.tolist()
+    nodes, tris, ext, shadow, nonfinite = cnt.tolist()
 
     for _ in range(args.warmup):
         step()
@@ -337,7 +337,8 @@ def main():
                              "divergence, not by HBM"},
             "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),
                                 "ext_queries": round(ext / samples_per_step, 3),
-                                "shadow_queries": round(shadow / samples_per_step, 3)},
+                                "shadow_queries": round(shadow / samples_per_step, 3),
+                                "nonfinite_samples": int(nonfinite)},
             "cpu_baseline": cpu,
             "cpu_numpy": cpu_np,
             "l2_vs_cpu": l2,

@@ -190,7 +190,9 @@ int prt_scene_kernel(void* scene, int32_t* out4);
 int prt_last_stats(void* scene, uint64_t* stats4);
 /* diagnostic words of the same call (16 x u64): the 4 counters above, then
  * wave-level shader clocks spent in work refill / traversal / shading, wave
- * loop iterations, and active lanes summed over iterations */
+ * loop iterations, and active lanes summed over iterations; [11] [12] lane-level
+ * inner / leaf traversal trips, [13] deepest traversal stack, [14] samples whose
+ * radiance came out NaN or infinite (failure detection; 0 for a sound scene) */
 int prt_diag_stats(void* scene, uint64_t* stats16);
 
 #ifdef __cplusplus

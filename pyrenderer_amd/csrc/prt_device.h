@@ -248,7 +248,7 @@ __device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, f
 }
 
 // ---------------------------------------------------------------- traversal
-struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp; };
+struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp, nonfinite; };
 
 // Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
 // t = (lo - o) / d is evaluated as fma(lo, 1/d, -o/d): pruning only, so the few-ulp
@@ -897,7 +897,7 @@ void trace_kernel(TraceParams P) {
     V3 mis_n = v3(0, 0, 0), mis_n2 = v3(0, 0, 0), mis_fl = v3(0, 0, 0), mis_bd = v3(0, 0, 0);
     float mis_bp = 0.0f;
     float tmax = kTMax;
-    Counters cn = {0, 0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
     uint32_t chunk_s = 0;   // wave-uniform: sample index (within the launch) of the current chunk
     uint32_t chunk_xy0 = 0; // wave-uniform: origin of the current chunk's tile
@@ -1296,6 +1296,8 @@ void trace_kernel(TraceParams P) {
         if (finished) {
             float* out = P.out + (size_t)item * 3;
             out[0] = L.x; out[1] = L.y; out[2] = L.z;
+            // failure detection (STATS): samples whose radiance is NaN or infinite
+            if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
             item = -1;
         }
         if (STATS) {
@@ -1323,6 +1325,9 @@ void trace_kernel(TraceParams P) {
             uint32_t m = cn.max_sp;
             for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_down((int)m, off));
             if (lane == 0) atomicMax(P.stats + 13, (unsigned long long)m);
+            uint32_t nf = cn.nonfinite;
+            for (int off = 32; off > 0; off >>= 1) nf += (uint32_t)__shfl_down((int)nf, off);
+            if (lane == 0 && nf) atomicAdd(P.stats + 14, (unsigned long long)nf);
         }
         {
             uint64_t a2 = l_inner, b2 = l_leaf;

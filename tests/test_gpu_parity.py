@@ -350,3 +350,27 @@ def test_mis_variant_on_a_global_scene_matches_oracle(cornell):
     g, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 2, 8, 6, N.PRT_FLAG_MIS_NEE)
     np.testing.assert_array_equal(g, o)
     ds.close()
+
+
+def test_nonfinite_sample_counter(gpu_scene, cornell):
+    """Failure detection: the STATS pass counts samples whose radiance is NaN or
+    infinite — none for the Cornell box; every sample that reaches a wall whose albedo is
+    NaN once the NaN guard cannot help (tracing.py:146-148 retries only with pdf = 1e-4)."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    from pyrenderer_amd.flatten import FlatScene
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    ids = np.arange(4, dtype=np.int32)
+    gpu_scene.render_tiles(cam, 64, 64, 32, 32, ids, 2, 8, 1, N.PRT_FLAG_STATS)
+    assert gpu_scene.diag_stats()[14] == 0
+    f = cornell[2]
+    mat = f.mat.copy()
+    mat[f.tri_mat[0], 0] = np.nan                  # the floor's red albedo
+    bad = FlatScene(f.tri_v, f.tri_n, f.tri_mat, f.tri_prim, f.prim_lo, f.prim_hi, mat, f.light_tri, f.light_off,
+                    f.direct_rgb)
+    ds = DeviceScene(bad, 0)
+    s, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 2, 8, 1, N.PRT_FLAG_STATS)
+    n_bad = int(ds.diag_stats()[14])
+    px_bad = int((~np.isfinite(s)).any(axis=1).sum())
+    assert n_bad > 0 and n_bad >= px_bad > 0, (n_bad, px_bad)
+    ds.close()
