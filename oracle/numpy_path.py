@@ -14,7 +14,8 @@ rounding per operation, the reference's expression order, the PCG streams keyed 
 bit-identical to the C oracle and therefore to the HIP kernel
 (tests/test_numpy_path.py).
 
-Scope: triangle scenes with Lambertian and light BSDFs (BASELINE configs 1, 2 and 5),
+Scope: triangle scenes (<= 4096 triangles) with Lambertian and light BSDFs (BASELINE configs 1,
+2 and 5),
 pinhole cameras; closest hit by brute force over all triangles (closest (t, index),
 which is what every backend of the oracle returns).  Specular BSDFs, spheres and thin
 lenses raise NotImplementedError.
@@ -37,6 +38,7 @@ K_PI_OVER_4 = F(0.78539816339744830961)
 K_TMIN = F(0.00001)
 K_TMAX = F(99999.9)
 MAX_F = F(3.402823466e+38)
+MAX_TRIANGLES = 4096   # brute force: Cornell-class scenes only
 _S = (F(-1.9515295891e-4), F(8.3321608736e-3), F(1.6666654611e-1))
 _C = (F(2.443315711809948e-5), F(1.388731625493765e-3), F(4.166664568298827e-2))
 
@@ -167,6 +169,9 @@ class NumpyScene:
         sph = g.get("sph")
         if sph is not None and np.asarray(sph).reshape(-1, 4).shape[0]:
             raise NotImplementedError("numpy path: spheres (config 3) are out of its scope")
+        if self.v0.shape[0] > MAX_TRIANGLES:
+            raise NotImplementedError(f"numpy path: brute-force closest hit over {self.v0.shape[0]} triangles "
+                                      f"(> {MAX_TRIANGLES}; config 4) is out of its scope")
         if np.any((self.mat[:, 5] == 2.0) | (self.mat[:, 5] == 3.0)):
             raise NotImplementedError("numpy path: metal / dielectric BSDFs (config 3) are out of its scope")
 

@@ -1010,6 +1010,9 @@ void trace_kernel(TraceParams P) {
             }
             t_a = t_b;
         }
+        // the leaf-phase entry / exit thresholds (counts of lanes) are tuned for full waves; in
+        // the drain, with few lanes left, they would switch phase after every trip
+        const int lb = exhausted ? 0 : P.leaf_break, le = exhausted ? 0 : P.leaf_exit;
         if (TRAV == 0) {
             if (qtype == Q_EXT) hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
             else hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
@@ -1019,30 +1022,34 @@ void trace_kernel(TraceParams P) {
             hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
         } else if (TRAV == 3 && RESUME) {
             if (!pending) tstate_init(tst, stk, tmax);
+            // suspending a query only pays while idle lanes can be refilled: once the work
+            // queue is exhausted (the launch's drain) the wave keeps traversing instead of
+            // going round the loop once per inner/leaf phase
+            const int res_min = exhausted ? 0 : P.resume_min;
             bool done;
             if (PHASE && do_shadow)
                 done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn,
-                                                                  &tst, P.resume_min, P.fault, P.leaf_break, P.leaf_exit);
+                                                                  &tst, res_min, P.fault, lb, le);
             else if (PHASE)
                 done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht,
-                                                                  cn, &tst, P.resume_min, P.fault, P.leaf_break, P.leaf_exit);
+                                                                  cn, &tst, res_min, P.fault, lb, le);
             else
                 done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk,
-                                                                  hid, ht, cn, &tst, P.resume_min, P.fault, P.leaf_break, P.leaf_exit);
+                                                                  hid, ht, cn, &tst, res_min, P.fault, lb, le);
             pending = !done;
             if (pending) continue;   // resume next iteration; no shading yet
             hit = hid >= 0;
         } else if (TRAV == 3 && PHASE) {
-            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
-            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
+            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
+            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
         } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
         } else {
             park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
             park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
             park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
             asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, P.leaf_break, P.leaf_exit);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
             asm volatile("" ::: "memory");
             float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
             beta = v3(k0.x, k0.y, k0.z);

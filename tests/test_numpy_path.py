@@ -43,3 +43,11 @@ def test_scope_is_enforced():
                 direct_rgb=np.ones(3, np.float32))
     with pytest.raises(NotImplementedError):
         NP.NumpyScene(flat)
+
+
+def test_large_scenes_are_out_of_scope():
+    big = dict(tri_v=np.zeros((NP.MAX_TRIANGLES + 1, 9), np.float32), tri_n=np.zeros((NP.MAX_TRIANGLES + 1, 3), np.float32),
+               tri_mat=np.zeros(NP.MAX_TRIANGLES + 1, np.int32), mat=np.array([[1, 1, 1, 0, 0, 0, 1.5, 0]], np.float32),
+               light_tri=np.zeros(1, np.int32), light_off=np.array([0, 1], np.int32), direct_rgb=np.ones(3, np.float32))
+    with pytest.raises(NotImplementedError):
+        NP.NumpyScene(big)
