@@ -95,3 +95,30 @@ def test_cli_arguments():
     assert a.scene == DEFAULT_SCENE and a.samples == 64 and a.depth == 16 and a.devices == [0]
     a = parse(["x.json", "--samples", "8", "--devices", "0", "1", "--nee", "mis", "--resolution", "64", "32"])
     assert a.samples == 8 and a.devices == [0, 1] and a.nee == "mis" and a.resolution == [64, 32]
+
+
+def test_tone_maps_restate_the_reference():
+    """finish = sqrt(pixels / samples) (main_taichi.py:61-64); reinhard_extended = the
+    extended Reinhard of main_taichi.py:67-78 / tone_map.py:17-35 on the mean radiance
+    (luminance 0.2126 / 0.7152 / 0.0722, white point = max luminance, zero-luminance pixels
+    stay black as tone_map.py:31-32 leaves them)."""
+    from pyrenderer_amd.tone_map import finish, luminance, reinhard_extended
+    rng = np.random.default_rng(5)
+    spp = 16
+    pixels = (rng.random((24, 20, 3)) * 40).astype(np.float32)
+    pixels[3, 4] = 0.0
+    mean = pixels / np.float32(spp)
+    np.testing.assert_array_equal(finish(mean), np.sqrt(pixels / np.float32(spp)))
+    lum = (mean[..., 0] * np.float32(0.2126) + mean[..., 1] * np.float32(0.7152)) + mean[..., 2] * np.float32(0.0722)
+    np.testing.assert_allclose(luminance(mean), lum, rtol=1e-6)
+    ref = np.zeros_like(mean, dtype=np.float64)
+    mw = float(lum.max())
+    for i in range(mean.shape[0]):
+        for j in range(mean.shape[1]):
+            li = float(lum[i, j])
+            if li == 0.0:
+                continue
+            l_new = li * (1.0 + li / (mw * mw)) / (1.0 + li)
+            ref[i, j] = pixels[i, j].astype(np.float64) * (l_new / li) / spp
+    np.testing.assert_allclose(reinhard_extended(mean), ref, rtol=2e-6, atol=1e-7)
+    assert not reinhard_extended(mean)[3, 4].any()
