@@ -1,7 +1,7 @@
 """Benchmark: Msamples/s of the path-tracing hot path, Cornell box 512x512 x 64 spp,
 depth 8 (BASELINE.json configs[1]), on N GPUs of one node.
 
-One step = one full frame: every rank renders its interleaved 64x64 tiles
+One step = one full frame: every rank renders its interleaved tiles (64x64 on one GPU, 16x16 on several)
 (device_scene.tile_owner, 'latin' scheme) through libprt's HIP path into a device
 buffer, then the per-tile radiance sums are gathered to rank 0 over RCCL
 (torch.distributed 'nccl' backend).  Total work is fixed as N grows ("scaling":
@@ -78,7 +78,9 @@ def parse():
     ap.add_argument("--res", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None)
-    ap.add_argument("--tile", type=int, default=64)
+    ap.add_argument("--tile", type=int, default=None,
+                    help="tile side in pixels (default 64 on one GPU, 16 on several: the finer latin "
+                         "interleave balances 8 ranks best, profiles/r01/shard_sim_c2_tiles_streams3.jsonl)")
     ap.add_argument("--streams", type=int, default=0,
                     help="frames in flight (1 = strictly serial frames; 0 = auto: 1, or 3 when a rank renders "
                          "< 8 M samples per frame, where the launch tail is a larger share)")
@@ -217,7 +219,7 @@ def main():
     ds = DeviceScene(flat, dev.index)
     t_build = time.perf_counter() - t_build
     W = H = args.res
-    T = args.tile
+    T = args.tile if args.tile else (64 if world == 1 else 16)
     n_streams = args.streams
     if n_streams <= 0:
         # measured (profiles/r01/shard_sim_*, streams_ab): for a whole C2 frame on one GPU,
