@@ -228,8 +228,10 @@ def main():
         # rocprof average it is checked against) would no longer be the kernel's own; serial
         # frames keep them equal.  For the 1/4 and 1/8 frames of 4- and 8-rank runs the launch
         # tail is a larger share: 3 frames in flight (0.741 vs 0.777 ms per frame at 1/8).
+        # On several GPUs the per-launch roofline is not the headline, and overlap pays more (a
+        # half frame at N = 2: 2.55 vs 2.65 ms with 2 streams, profiles/r01/shard_sim_c2_streams_t16.jsonl).
         rank_samples = W * H * args.spp / world
-        n_streams = 1 if rank_samples >= 8e6 else 3
+        n_streams = 3 if rank_samples < 8e6 else (2 if world > 1 else 1)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
     shards = [TileShard(W, H, T, rank, world, dev, args.scheme) for _ in range(n_streams)]
     my_tiles = shards[0].tiles
