@@ -8,7 +8,8 @@ buffer, then the per-tile radiance sums are gathered to rank 0 over RCCL
 "strong").  Consecutive frames alternate between --streams HIP streams, each with
 its own buffers, so the drain of frame k (the last paths of a persistent launch,
 ~0.3 ms at any frame size) and its gather overlap the start of frame k+1 (auto: 3
-streams when a rank renders < 8 M samples per frame, else serial frames).
+streams when a rank renders < 8 M samples per frame, else 2 on several GPUs and
+serial frames on one, where the per-launch roofline is measured).
 
     python bench.py --gpus 1 --steps 10 --warmup 3
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
@@ -82,8 +83,8 @@ def parse():
                     help="tile side in pixels (default 64 on one GPU, 16 on several: the finer latin "
                          "interleave balances 8 ranks best, profiles/r01/shard_sim_c2_tiles_streams3.jsonl)")
     ap.add_argument("--streams", type=int, default=0,
-                    help="frames in flight (1 = strictly serial frames; 0 = auto: 1, or 3 when a rank renders "
-                         "< 8 M samples per frame, where the launch tail is a larger share)")
+                    help="frames in flight (1 = strictly serial frames; 0 = auto: 3 when a rank renders < 8 M "
+                         "samples per frame, else 2 on several GPUs and 1 on one)")
     ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
