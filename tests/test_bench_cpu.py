@@ -1,0 +1,48 @@
+"""bench.py's host-side contract, checked without a GPU: defaults (config 2 = BASELINE's
+configs[1]), the CPU legs' report formats and the per-pixel comparison arithmetic."""
+import sys
+import types
+
+import numpy as np
+
+from conftest import ROOT
+
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_defaults_are_the_baseline_workload(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.config, a.scene, a.res, a.spp, a.depth) == (2, "cornell", 512, 64, 8)
+    assert a.steps > 0 and a.warmup >= 0 and a.tile is None and a.streams == 0
+    assert sorted(bench.CONFIGS) == [1, 2, 3, 4, 5]
+    assert bench.CONFIGS[5]["res"] == 4096 and bench.CONFIGS[5]["spp"] == 256
+
+
+def test_l2_vs_cpu_arithmetic():
+    args = types.SimpleNamespace(res=16, spp=4)
+    ids = np.array([0, 3], np.int32)
+    rng = np.random.default_rng(0)
+    frame = rng.random((16, 16, 3)).astype(np.float32)
+    tx = 16 // 8
+    cpu = np.stack([frame[(t % tx) * 8:(t % tx) * 8 + 8, (t // tx) * 8:(t // tx) * 8 + 8].transpose(1, 0, 2)
+                    for t in ids]).reshape(-1, 3)
+    r = bench.l2_vs_cpu(frame, ids, cpu, args)
+    assert r["identical_pixels"] == 1.0 and r["rmse"] == 0.0 and r["pass"]
+    cpu2 = cpu.copy()
+    cpu2[5, 1] += 0.04                      # one pixel off by 0.01 in mean radiance
+    r = bench.l2_vs_cpu(frame, ids, cpu2, args)
+    assert r["pixels"] == 128 and abs(r["max_pixel_l2"] - 0.01) < 1e-6 and not r["pass"]
+
+
+def test_cpu_leg_reports():
+    args = types.SimpleNamespace(res=64, spp=2, depth=4, seed=1)
+    c = bench.cpu_baseline(np.arange(10000), 2.0, 4, args)
+    assert c["kind"] == "port" and c["cores"] == 4 and c["unit"] == "Msamples/s"
+    assert c["value"] == round(10000 * 64 * 2 / 2.0 / 1e6, 4)
+    scene, cam = bench.load_scene("cornell")
+    from pyrenderer_amd.flatten import flatten_scene
+    rep, ids, sums = bench.numpy_baseline(flatten_scene(scene), cam.convert_to_taichi_camera().packed(), args, 0.2)
+    assert rep["kind"] == "port" and rep["value"] > 0 and sums.shape == (len(ids) * 64, 3)
