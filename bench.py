@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+LDS_PEAK_GBS = 150000.0  # MI355X_MICROARCH.md §LDS: ~150 TB/s aggregate for ds_read_b128 at ~2.4 GHz
 VALU_PEAK_TFLOPS = 157.3
 # Algorithmic bytes per unit of work: one BVH node record
 # (two child boxes + refs), one triangle record (v0, e1, e2 + id), one light
@@ -292,6 +293,10 @@ def main():
         bytes_launch = ((b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank
                         + B_SAMPLE * n_px_rank * args.spp + B_PIXEL * n_px_rank) / launches_per_step
         achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
+        # the scene part of those bytes (nodes, triangles, light records): LDS reads for an
+        # LDS-resident scene
+        scene_gbs = ((b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank / launches_per_step
+                     / (kern_avg_ms * 1e-3) / 1e9)
         flops_launch = (F_BOX * arity * nodes + F_TRI * tris) * per_rank / launches_per_step
         traffic, pmc = None, {}
         if args.pmc_json and os.path.exists(args.pmc_json) and world == 1:
@@ -340,6 +345,11 @@ def main():
                      "note": "achieved = counted box/triangle flops; issue_util / lane_util from the committed "
                              "SQ counter pass (profiles/pmc.json): the kernel is bound by VALU issue under "
                              "divergence, not by HBM"},
+            "lds": ({"achieved": round(scene_gbs, 2), "peak": LDS_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(scene_gbs / LDS_PEAK_GBS, 4),
+                     "note": "LDS-resident scene: the algorithmic node/triangle bytes are LDS reads, so this, "
+                             "not HBM, is the memory roofline they are served against"}
+                    if kinfo["lds_scene"] else None),
             "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),
                                 "ext_queries": round(ext / samples_per_step, 3),
                                 "shadow_queries": round(shadow / samples_per_step, 3),
