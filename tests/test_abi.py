@@ -138,3 +138,14 @@ def test_window_and_multi_argument_errors_without_gpu():
     assert b"NULL" in L.prt_last_error()
     L.prt_comm_release()   # no communicator yet: a no-op
 
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No CPU fallback: without libprt.so every product entry point raises."""
+    from pyrenderer_amd import _native as N
+    monkeypatch.setattr(N, "LIB", str(tmp_path / "libprt.so"))
+    monkeypatch.setattr(N, "_lib", None)
+    with pytest.raises(N.PrtError, match="not found"):
+        N.lib()
+    with pytest.raises(N.PrtError):
+        N.device_count()
