@@ -374,3 +374,26 @@ def test_nonfinite_sample_counter(gpu_scene, cornell):
     px_bad = int((~np.isfinite(s)).any(axis=1).sum())
     assert n_bad > 0 and n_bad >= px_bad > 0, (n_bad, px_bad)
     ds.close()
+
+
+def test_mis_variant_on_the_specular_scene():
+    """MIS estimator with config 3's materials: its closest-hit visibility queries also land
+    on the analytic sphere (hit ids >= n_tri, sphere material lookup) and on specular boxes."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    scene, cam, flat = _specular_scene(0.35)
+    ds = DeviceScene(flat, 0)
+    osc = O.OracleScene.from_flat(flat)
+    c = cam.convert_to_taichi_camera().packed()
+    ids = np.arange(4, dtype=np.int32)
+    O.set_nee_mode(True)
+    try:
+        o = osc.render_tiles(c, 64, 64, 32, 32, ids, 4, 8, seed=12)
+    finally:
+        O.set_nee_mode(False)
+    g, _ = ds.render_tiles(c, 64, 64, 32, 32, ids, 4, 8, 12, N.PRT_FLAG_MIS_NEE)
+    assert np.isfinite(g).all() and g.sum() > 0
+    rmse, same = _compare(g, o, 4)
+    assert rmse < TOL_RMSE, rmse
+    assert same >= 0.999, same
+    ds.close()
