@@ -47,13 +47,13 @@ extern "C" {
  * sample_direct_lighting — two closest-hit visibility queries per diffuse vertex (light
  * and BRDF strategies, power heuristic, light_area 1.0 as the reference passes it).
  * A different estimator: the image differs from the default one (oracle: or_set_nee_mode).
- * Selects the MIS kernel variants (32, 33); an explicit variant must agree with the flag. */
+ * Selects the MIS kernel variants (4, 5); an explicit variant must agree with the flag. */
 #define PRT_FLAG_MIS_NEE 0x8u
 /* trace-kernel variant in bits 8..15 (0 = automatic; the numbering is the
- * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: split / unified / while-while
- * traversal, BVH2 / BVH4, global / LDS-resident scene, occupancy targets,
- * phase-aligned scheduling).  All variants produce bit-identical images; the
- * selector exists for A/B runs. */
+ * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: 1 LDS-resident scene, 2 the same
+ * without an occupancy target, 3 global scene (quantised nodes, spill stack), 4 / 5 the
+ * MIS estimator on an LDS / global scene).  Variants of one estimator produce
+ * bit-identical images; the selector exists for A/B runs and tests. */
 #define PRT_FLAG_VARIANT_SHIFT 8
 #define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFFu) << PRT_FLAG_VARIANT_SHIFT)
 
@@ -173,6 +173,12 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
  * traversal watchdog tripped in the last render (device-output renders are not
  * checked otherwise). */
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
+/* Failure detection for renders whose result stays on the device (prt_render_tiles_device,
+ * the torch.distributed path): synchronises the device, then reports PRT_ERR_INTERNAL if
+ * the traversal watchdog tripped in the last render enqueued on any of this scene's
+ * streams (or in the last prt_closest_hits call).  PRT_OK otherwise.  The host-output
+ * entry points check the flag themselves. */
+int prt_check_faults(void* scene);
 /* World.hit_all for a batch of rays (mathematics/intersection_taichi.py:238-291):
  * rays = n x 8 f32 (o.xyz, t_min, d.xyz, t_max); hit_id = original triangle index,
  * n_tri + k for sphere k, -1 for a miss; hit_t = distance (0 on a miss).  Closest hit

@@ -11,16 +11,18 @@ import numpy as np
 from .build import LIB
 
 PRT_OK = 0
+PRT_ERR_INTERNAL = -6   # device-side check failed (traversal watchdog)
 PRT_FLAG_STATS = 0x1
 PRT_FLAG_TIME = 0x2
 PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
 PRT_FLAG_MIS_NEE = 0x8
-# trace-kernel variant ids 1..VAR_LAST of the reference estimator (pyrenderer_amd/csrc/prt_kernels.h);
-# the MIS direct-lighting estimator's variants (PRT_FLAG_MIS_NEE) follow
-VAR_LAST = 31
-VAR_MIS = (32, 33)
-VAR_WW4_PH_LDS6 = 15
-VAR_WW4_Q_SP5 = 23
+# trace-kernel variant ids 1..VAR_LAST of the reference estimator (pyrenderer_amd/csrc/prt_kernels.h
+# kVar*); the MIS direct-lighting estimator's variants (PRT_FLAG_MIS_NEE) follow
+VAR_LDS = 1           # LDS-resident scene, phase-aligned schedule, >= 6 waves/SIMD
+VAR_LDS_ANY_OCC = 2   # ... without the occupancy target
+VAR_GLOBAL = 3        # scene in HBM: quantised BVH4, LDS stack + global spill, suspended tails
+VAR_LAST = 3
+VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 
@@ -60,6 +62,7 @@ EXPORTS = {
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_tiles_accumulate": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_kernel_timing": (_i, [_vp, _vp, _vp]),
+    "prt_check_faults": (_i, [_vp]),
     "prt_last_stats": (_i, [_vp, _vp]),
     "prt_diag_stats": (_i, [_vp, _vp]),
 }

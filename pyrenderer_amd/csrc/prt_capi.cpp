@@ -102,18 +102,17 @@ struct Scene {
     int64_t n_tri = 0;
     int64_t n_nodes = 0;
     int32_t depth = 0;
-    int stack = 16;
     int n_light = 0;
     int n_mat = 0;
     int cus = 0;
     int blocks_per_cu = 0;           // of the default variant
     int occ[2 * (prt::kVarLast + 1)] = {0};  // blocks/CU per (variant, stats) once queried
     int n_lt = 0;                    // emitter triangles
-    int64_t n_node_f4 = 0, n_tri_f4 = 0;
+    int64_t n_tri_f4 = 0;
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
     DevBuf nodes4q;                  // quantised BVH4 (prt_internal.h)
     int64_t n_node4q_f4 = 0;
-    DevBuf nodes, nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
+    DevBuf nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
     int64_t n_node4_f4 = 0;
     int32_t depth4 = 0;
     int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
@@ -121,6 +120,7 @@ struct Scene {
     int leaf_break = -1;             // env PRT_LEAF_BREAK (0..64); -1: per variant (trace launch)
     int leaf_exit = 8;               // env PRT_LEAF_EXIT (0..64); C2 5.25 -> 5.04 ms, C4 29.8 -> 28.8 ms
     int resume_min = 48;             // resume variants (env PRT_RESUME_MIN; C4 sweep: 16 -> 37.4 ms, 48 -> 34.8 ms)
+    uint32_t guard_trips = 1u << 20; // traversal phases per query before the watchdog trips (env PRT_GUARD_TRIPS)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
     int64_t n_sph = 0;
     DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
@@ -153,7 +153,7 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->nodes4q, &s->nodes, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v,
+    for (DevBuf* b : {&s->nodes4q, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v,
                       &s->light_off, &s->sph, &s->sph_mat, &s->work, &s->stats, &s->frame, &s->gather,
                       &s->gather_xy})
         b->release();
@@ -229,35 +229,35 @@ RenderCtx* ctx_for(Scene* s, hipStream_t stream) {
 
 // LDS-resident scene: BVH + triangles small enough to sit beside the stack
 constexpr int64_t kLdsSceneBytes = 24 * 1024;
-void scene_sizes(const Scene* s, bool bvh4, prt::TraceParams& P) {
-    P.n_node_f4 = (int)(bvh4 ? s->n_node4_f4 : s->n_node_f4);
+void scene_sizes(const Scene* s, prt::TraceParams& P) {
+    P.n_node_f4 = (int)s->n_node4_f4;
     P.n_tri_f4 = (int)s->n_tri_f4;
     P.n_tri = (int)s->n_tri;
     P.n_mat = s->n_mat;
     P.n_lt = s->n_lt;
     P.n_light = s->n_light;
 }
-bool lds_fits_var(const Scene* s, bool bvh4) {
+bool lds_fits4(const Scene* s) {
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
-    scene_sizes(s, bvh4, P);
+    scene_sizes(s, P);
     return (int64_t)prt::lds_scene_bytes(P) <= kLdsSceneBytes;
 }
-bool lds_fits(const Scene* s) { return lds_fits_var(s, false); }
-bool lds_fits4(const Scene* s) { return lds_fits_var(s, true); }
 // LDS-resident scene when it fits; the >= 6 waves/SIMD build when six blocks' LDS
 // still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
+// Everything else (and BVH4s deeper than the 64-entry LDS stack) takes the global-scene
+// kernel: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal tails,
+// >= 6 waves/SIMD (C4: 28.6 ms at 5 waves, 27.2 at 6, 28.6 at 7 with spills).
 int default_variant(const Scene* s) {
-    // global scene: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal
-    // tails, >= 6 waves/SIMD (C4: 28.6 ms at 5 waves, 27.2 at 6, 28.6 at 7 with spills)
-    if (!lds_fits4(s)) return prt::kVarWW4QRSp6;
-    if (!s->stack4) return prt::kVarWW;
+    if (!lds_fits4(s) || !s->stack4) return prt::kVarGlobal;
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
-    scene_sizes(s, true, P);
-    size_t smem = prt::trace_smem_bytes(s->stack4, prt::kVarWW4Lds6, P);
-    return smem * 6 <= 160 * 1024 ? prt::kVarWW4PhLds6 : prt::kVarWW4Lds;
+    scene_sizes(s, P);
+    size_t smem = prt::trace_smem_bytes(s->stack4, prt::kVarLds, P);
+    return smem * 6 <= 160 * 1024 ? prt::kVarLds : prt::kVarLdsAnyOcc;
 }
+// the traversal stack entries of variant `var` (LDS part for the spill variants)
+int variant_stack(const Scene* s, int var) { return prt::variant_spills(var) ? s->spill_lds : s->stack4; }
 
 // Pinhole camera with an affine matrix (no aperture, last row (0,0,0,1), all finite):
 // the kernels may use the exact gen_ray shortcut (TraceParams::cam_fast).
@@ -312,7 +312,7 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
 
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
-    P.nodes = (const float4*)s->nodes.p;
+    P.nodes = (const float4*)s->nodes4.p;
     P.tris = (const float4*)s->tris.p;
     P.tri_nm = (const float4*)s->tri_nm.p;
     P.tri_frame = (const float4*)s->tri_frame.p;
@@ -345,32 +345,25 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     P.fault = (int*)((char*)cx->work.p + kFaultOffset);
     P.out = (float*)cx->buf.p;
     P.stats = (unsigned long long*)s->stats.p;
-    scene_sizes(s, false, P);
-    int stack = s->stack;
+    scene_sizes(s, P);
+    P.guard_trips = s->guard_trips;
     P.n_sph = (int)s->n_sph;
     P.sph = (const float4*)s->sph.p;
     P.sph_mat = (const int*)s->sph_mat.p;
     int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFFu);
     const bool mis = (flags & PRT_FLAG_MIS_NEE) != 0;
-    if (var == 0)
-        var = !mis ? default_variant(s) : (lds_fits4(s) && s->stack4) ? prt::kVarWW4Lds6Mis : prt::kVarWW4QRSp6Mis;
-    if (var < prt::kVarSplit || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
+    if (var == 0) var = !mis ? default_variant(s) : (lds_fits4(s) && s->stack4) ? prt::kVarLdsMis : prt::kVarGlobalMis;
+    if (var < prt::kVarFirst || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
     if (prt::variant_mis(var) != mis)
         return fail(PRT_ERR_ARG, "PRT_FLAG_MIS_NEE must be set exactly for the MIS estimator variants");
-    const bool b4 = prt::variant_uses_bvh4(var);
     const bool spill = prt::variant_spills(var);
-    if (b4) {
-        if (s->stack4 == 0 && !spill) return fail(PRT_ERR_ARG, "BVH4 too deep for the traversal stack variants");
-        P.nodes = (const float4*)s->nodes4.p;
-        P.n_node_f4 = (int)s->n_node4_f4;
-        stack = spill ? s->spill_lds : s->stack4;
-        if (prt::variant_quantized(var)) {
-            P.nodes = (const float4*)s->nodes4q.p;
-            P.n_node_f4 = (int)s->n_node4q_f4;
-        }
+    if (s->stack4 == 0 && !spill) return fail(PRT_ERR_ARG, "BVH4 too deep for the LDS traversal stack variants");
+    const int stack = variant_stack(s, var);
+    if (prt::variant_quantized(var)) {
+        P.nodes = (const float4*)s->nodes4q.p;
+        P.n_node_f4 = (int)s->n_node4q_f4;
     }
-    if (prt::variant_uses_lds(var) && !(b4 ? lds_fits4(s) : lds_fits(s)))
-        return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
+    if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
     // while-while leaf-phase entry: LDS scenes wait for every descending lane's leaf (their
     // leaves are cheap and traversals short); global scenes enter the leaf phase once at
     // most 8 descending lanes still lack one (C4: 35.1 -> 29.7 ms; C2 prefers 0)
@@ -576,7 +569,6 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
     s->n_tri = n_tri;
     s->n_nodes = bvh.n_nodes;
     s->depth = bvh.depth;
-    s->stack = prt::stack_variant(bvh.depth);
     s->n_light = n_light;
     s->n_mat = n_mat;
     if (direct_rgb) std::memcpy(s->direct_rgb, direct_rgb, sizeof(float) * 3);
@@ -609,7 +601,6 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             }
             lv[16 * k + 15] = bits_f(tri_mat[t]);
         }
-        if ((rc = upload(s->nodes, bvh.nodes.data(), sizeof(float) * bvh.nodes.size(), &s->device_bytes))) break;
         {
             prt::Bvh4Host b4;
             prt::collapse_bvh4(bvh, &b4);
@@ -639,10 +630,11 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) { rc = fail(PRT_ERR_HIP, hipGetErrorString(e)); break; }
         s->cus = prop.multiProcessorCount;
-        s->n_node_f4 = (int64_t)bvh.nodes.size() / 4;
         s->n_tri_f4 = (int64_t)bvh.tris.size() / 4;
         if (const char* le = std::getenv("PRT_LEAF_EXIT")) s->leaf_exit = std::max(0, std::min(64, std::atoi(le)));
         if (const char* lb = std::getenv("PRT_LEAF_BREAK")) s->leaf_break = std::max(0, std::min(64, std::atoi(lb)));
+        if (const char* gt = std::getenv("PRT_GUARD_TRIPS"))
+            s->guard_trips = (uint32_t)std::max(1LL, std::min((long long)UINT32_MAX, std::atoll(gt)));
         if (const char* rm = std::getenv("PRT_RESUME_MIN")) s->resume_min = std::max(1, std::min(64, std::atoi(rm)));
         if (const char* sl = std::getenv("PRT_SPILL_LDS")) {
             int v = std::atoi(sl);
@@ -652,9 +644,8 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             prt::TraceParams Q;
             std::memset(&Q, 0, sizeof(Q));
             int var = default_variant(s);
-            bool b4 = prt::variant_uses_bvh4(var);
-            scene_sizes(s, b4, Q);
-            int stk = prt::variant_spills(var) ? s->spill_lds : b4 ? s->stack4 : s->stack;
+            scene_sizes(s, Q);
+            int stk = variant_stack(s, var);
             s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(stk, var, false, prt::trace_smem_bytes(stk, var, Q)));
         }
         if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
@@ -668,7 +659,7 @@ int prt_scene_info(void* scene, int64_t* info8) {
     auto* s = (Scene*)scene;
     if (!s || !info8) return fail(PRT_ERR_ARG, "NULL argument");
     info8[0] = s->device; info8[1] = s->n_tri; info8[2] = s->n_nodes; info8[3] = s->depth;
-    info8[4] = s->stack; info8[5] = (int64_t)s->device_bytes; info8[6] = s->blocks_per_cu; info8[7] = s->cus;
+    info8[4] = s->stack4; info8[5] = (int64_t)s->device_bytes; info8[6] = s->blocks_per_cu; info8[7] = s->cus;
     return PRT_OK;
 }
 
@@ -692,6 +683,7 @@ int prt_closest_hits(void* scene, const float* rays, int64_t n, uint32_t flags, 
     HIP_TRY(d_id.ensure(sizeof(int32_t) * (size_t)n));
     HIP_TRY(d_t.ensure(sizeof(float) * (size_t)n));
     P.fault = (int*)((char*)s->work.p + kFaultOffset);
+    P.guard_trips = s->guard_trips;
     HIP_TRY(hipMemsetAsync(P.fault, 0, sizeof(int), s->stream));
     HIP_TRY(hipMemcpyAsync(d_rays.p, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice, s->stream));
     HIP_TRY(prt::launch_hits(P, quant, any, 64, (const float4*)d_rays.p, n, (int*)d_id.p, (float*)d_t.p, s->stream));
@@ -706,11 +698,10 @@ int prt_scene_kernel(void* scene, int32_t* out4) {
     auto* s = (Scene*)scene;
     if (!s || !out4) return fail(PRT_ERR_ARG, "NULL argument");
     int var = default_variant(s);
-    bool b4 = prt::variant_uses_bvh4(var);
     out4[0] = var;
-    out4[1] = b4 ? 4 : 2;
+    out4[1] = 4;
     out4[2] = (prt::variant_uses_lds(var) ? 1 : 0) | (prt::variant_quantized(var) ? 2 : 0);
-    out4[3] = prt::variant_spills(var) ? s->spill_lds : b4 ? s->stack4 : s->stack;
+    out4[3] = variant_stack(s, var);
     return PRT_OK;
 }
 
@@ -804,6 +795,18 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     }
     s->ev_used = 0;
+    return PRT_OK;
+}
+
+int prt_check_faults(void* scene) {
+    auto* s = (Scene*)scene;
+    if (!s) return fail(PRT_ERR_ARG, "NULL argument");
+    DeviceGuard g(s->device);
+    // every stream a render was enqueued on: the device-wide synchronisation also covers
+    // streams the caller owns (torch streams) without holding their handles past their life
+    HIP_TRY(hipDeviceSynchronize());
+    if (read_render_faults(s) != 0 || read_fault(s) != 0)
+        return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     return PRT_OK;
 }
 

@@ -250,114 +250,8 @@ __device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, f
 // ---------------------------------------------------------------- traversal
 struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp, nonfinite; };
 
-// Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
-// t = (lo - o) / d is evaluated as fma(lo, 1/d, -o/d): pruning only, so the few-ulp
-// error of the estimate is covered by the box padding (~1e-6 of the scene scale,
-// >> |o/d| ulp) and the 1+2*gamma3 factor on t_far.  The near and far plane of each
-// axis are chosen by the sign of 1/d, NOT by min/max of the two distances: for a
-// direction component of exactly 0 (1/d = inf) a plane distance can be NaN, and
-// fminf/fmaxf would then turn the other plane's -inf into the FAR distance and cull
-// a box the ray lies inside (measured: 8 of 262144 pixels at config 2).  With the
-// selection, a NaN distance is dropped by the fmaxf/fminf that follow, which can
-// only enlarge the interval.  sx/sy/sz: 1/d.{x,y,z} < 0.
-__device__ __forceinline__ bool slab(float lx, float hx, float ly, float hy, float lz, float hz, V3 oi, V3 inv,
-                                     float tmin, float tmax, float& tn) {
-    const bool sx = __float_as_int(inv.x) < 0, sy = __float_as_int(inv.y) < 0, sz = __float_as_int(inv.z) < 0;
-    float ax = __builtin_fmaf(lx, inv.x, -oi.x), bx = __builtin_fmaf(hx, inv.x, -oi.x);
-    float ay = __builtin_fmaf(ly, inv.y, -oi.y), by = __builtin_fmaf(hy, inv.y, -oi.y);
-    float az = __builtin_fmaf(lz, inv.z, -oi.z), bz = __builtin_fmaf(hz, inv.z, -oi.z);
-    float nx = sx ? bx : ax, fx = sx ? ax : bx;
-    float ny = sy ? by : ay, fy = sy ? ay : by;
-    float nz = sz ? bz : az, fz = sz ? az : bz;
-    float tnear = fmaxf(fmaxf(nx, ny), fmaxf(nz, tmin));
-    float tfar = fminf(fminf(fx, fy), fminf(fz, tmax)) * kGamma;   // min(a g, b g) = min(a, b) g (g > 0)
-    tn = tnear;
-    return tnear <= tfar;
-}
-
 // Moller-Trumbore in the reference's exact expression order
-// (intersection_taichi.py:69-91).  `accept(t)` decides the t-range part.
-template <bool ANY>
-__device__ __forceinline__ bool mt(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, float tbest, int id, int best_id,
-                                   float& tout) {
-    V3 c = cross(e1, d);
-    float det = dot(c, e2);
-    if (!(fabsf(det) > 0.0f)) return false;
-    float f = rcp_exact(det);
-    V3 s = o - v0;
-    V3 q = cross(s, e2);
-    float t = -f * dot(q, e1);
-    bool in_range = ANY ? (t0 < t && t < tbest) : (t0 < t && (t < tbest || (t == tbest && id < best_id)));
-    if (!in_range) return false;
-    float u = -f * dot(q, d);
-    if (!(0.0f <= u && u <= 1.0f)) return false;
-    float v = f * dot(c, s);
-    if (!(v >= 0.0f && 1.0f - u - v >= 0.0f)) return false;
-    tout = t;
-    return true;
-}
-
-// Closest hit (ANY=false) or any hit (ANY=true) over the BVH2.
-// lstack: this lane's LDS stack, entry k at lstack[k * kBlock].
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool traverse(const TraceParams& P, V3 o, V3 d, float tmin, float tmax, int* lstack,
-                                         int& hit_id, float& hit_t, Counters& cn) {
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    V3 oi = o * inv;
-    float best = tmax;
-    int best_id = -1;
-    int sp = 0;
-    int cur = 0;
-    while (true) {
-        if (cur >= 0) {
-            const float4* nd = P.nodes + (size_t)cur * 4;
-            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            if (STATS) cn.nodes++;
-            float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
-            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
-            if (hl && hr) {
-                bool lf = tl <= tr;
-                cur = lf ? cl : cr;
-                lstack[sp * kBlock] = lf ? cr : cl;
-                ++sp;
-            } else if (hl) {
-                cur = cl;
-            } else if (hr) {
-                cur = cr;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                cur = lstack[sp * kBlock];
-            }
-        } else {
-            int v = -cur - 1;
-            int first = v >> 3, cnt = (v & 7) + 1;
-            for (int k = 0; k < cnt; ++k) {
-                const float4* tp = P.tris + (size_t)(first + k) * 3;
-                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
-                int id = __float_as_int(t0.w);
-                float t;
-                if (STATS) cn.tris++;
-                if (mt<ANY>(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, t)) {
-                    best = t;
-                    best_id = id;
-                    if (ANY) { hit_id = id; hit_t = t; return true; }
-                }
-            }
-            if (sp == 0) break;
-            --sp;
-            cur = lstack[sp * kBlock];
-        }
-    }
-    hit_id = best_id;
-    hit_t = best;
-    return best_id >= 0;
-}
-
-// Unified traversal: one loop serves closest-hit (extension) and any-hit
-// (shadow) lanes of the same wave, so the two query kinds never serialise.
+// (intersection_taichi.py:69-91), for closest-hit and any-hit lanes of one wave.
 // nodes/tris point either to global memory or to the block's LDS copy of a
 // small scene (the compiler infers the address space after inlining).
 __device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, float tbest, int id, int best_id,
@@ -380,63 +274,6 @@ __device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, 
     return hit;
 }
 
-template <bool STATS>
-__device__ __forceinline__ bool traverse_u(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                           V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
-                                           float& hit_t, Counters& cn) {
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    V3 oi = o * inv;
-    float best = tmax;
-    int best_id = -1;
-    int sp = 0;
-    int cur = 0;
-    while (true) {
-        if (cur >= 0) {
-            const float4* nd = nodes + (size_t)cur * 4;
-            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            if (STATS) cn.nodes++;
-            float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
-            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
-            if (hl && hr) {
-                bool lf = tl <= tr;
-                cur = lf ? cl : cr;
-                lstack[sp * kBlock] = lf ? cr : cl;
-                ++sp;
-            } else if (hl | hr) {
-                cur = hl ? cl : cr;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                cur = lstack[sp * kBlock];
-            }
-        } else {
-            int v = -cur - 1;
-            int first = v >> 3, cnt = (v & 7) + 1;
-            bool done = false;
-            for (int k = 0; k < cnt; ++k) {
-                const float4* tp = tris + (size_t)(first + k) * 3;
-                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
-                int id = __float_as_int(t0.w);
-                float t;
-                if (STATS) cn.tris++;
-                if (mt_u(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, any, t)) {
-                    best = t;
-                    best_id = id;
-                    if (any) { done = true; break; }
-                }
-            }
-            if (done || sp == 0) break;
-            --sp;
-            cur = lstack[sp * kBlock];
-        }
-    }
-    hit_id = best_id;
-    hit_t = best;
-    return best_id >= 0;
-}
-
 // While-while traversal (Aila & Laine 2009, "persistent while-while"): lanes
 // descend inner nodes until every lane of the wave holds a postponed leaf,
 // then all lanes test leaf triangles together, so inner-node and leaf work
@@ -444,76 +281,6 @@ __device__ __forceinline__ bool traverse_u(const float4* __restrict__ nodes, con
 // holds kSentinel; leaves are negative references, inner nodes >= 0.
 constexpr int kSentinel = 0x7FFFFFFF;
 constexpr uint32_t kGuardTrips = 1u << 20;   // leaf batches per query before the watchdog trips
-
-template <bool STATS>
-__device__ __forceinline__ bool traverse_ww(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                            V3 d, float tmin, float tmax, bool any, int* lstack, int& hit_id,
-                                            float& hit_t, Counters& cn) {
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-    V3 oi = o * inv;
-    float best = tmax;
-    int best_id = -1;
-    lstack[0] = kSentinel;
-    int sp = 0;         // index of the top entry
-    int cur = 0;        // root
-    int leaf = 0;       // postponed leaf (< 0); >= 0 means none
-    do {
-        // --- inner nodes until all lanes have a postponed leaf
-        while (cur >= 0 && cur != kSentinel) {
-            const float4* nd = nodes + (size_t)cur * 4;
-            float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3];
-            if (STATS) { cn.nodes++; cn.it_inner++; }
-            float tl, tr;
-            bool hl = slab(a.x, a.y, a.z, a.w, b.x, b.y, oi, inv, tmin, best, tl);
-            bool hr = slab(b.z, b.w, c.x, c.y, c.z, c.w, oi, inv, tmin, best, tr);
-            int cl = __float_as_int(e.x), cr = __float_as_int(e.y);
-            if (!hl && !hr) {
-                cur = lstack[sp * kBlock];
-                --sp;
-            } else {
-                bool lf = hl && (!hr || tl <= tr);
-                cur = lf ? cl : cr;
-                if (hl && hr) {
-                    ++sp;
-                    lstack[sp * kBlock] = lf ? cr : cl;
-                }
-            }
-            if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
-                leaf = cur;
-                cur = lstack[sp * kBlock];
-                --sp;
-            }
-            if (!__any(leaf >= 0)) break;  // every lane holds a leaf: go test triangles
-        }
-        // --- leaves
-        while (leaf < 0) {
-            int v = -leaf - 1;
-            int first = v >> 3, cnt = (v & 7) + 1;
-            if (STATS) cn.it_leaf++;
-            for (int k = 0; k < cnt; ++k) {
-                const float4* tp = tris + (size_t)(first + k) * 3;
-                float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
-                int id = __float_as_int(t0.w);
-                float t;
-                if (STATS) cn.tris++;
-                if (mt_u(xyz(t0), xyz(t1), xyz(t2), o, d, tmin, best, id, best_id, any, t)) {
-                    best = t;
-                    best_id = id;
-                    if (any) { cur = kSentinel; break; }
-                }
-            }
-            if (any && best_id >= 0) { leaf = 0; break; }
-            leaf = cur;
-            if (cur < 0) {
-                cur = lstack[sp * kBlock];
-                --sp;
-            }
-        }
-    } while (cur != kSentinel || leaf < 0);
-    hit_id = best_id;
-    hit_t = best;
-    return best_id >= 0;
-}
 
 // While-while over the BVH4 (prt_internal.h): one node fetch tests four child
 // boxes; hit children are ordered near-to-far with a 5-comparator network, the
@@ -570,7 +337,7 @@ __device__ __forceinline__ float ubyte(uint32_t w, int k) {
 // Child k of a quantised node (prt_internal.h): plane distance (origin + q s - o) / d
 // evaluated as fma(q, s/d, (origin - o)/d); the >= 2 pad outward rounding of the grid
 // covers the estimate's error, so the test stays conservative.  The q words arrive
-// already swapped into near/far order by the sign of 1/d (see slab()).
+// already swapped into near/far order by the sign of 1/d (see slab_nf()).
 struct QAxis { float A, B; };
 __device__ __forceinline__ bool qchild(int k, uint32_t lxq, uint32_t hxq, uint32_t lyq, uint32_t hyq, uint32_t lzq,
                                        uint32_t hzq, QAxis X, QAxis Y, QAxis Z, float tmin, float tmax, float& tn) {
@@ -591,9 +358,17 @@ __device__ __forceinline__ void tstate_init(TState& ts, S stk, float tmax) {
 // traversing; the unfinished lanes keep their state (registers + LDS stack) and resume
 // in the next iteration, so the long tail of a few slow lanes no longer idles the
 // others.  Returns whether the query finished (hit_id / hit_t valid).
-// Slab test with the near/far planes already selected by the sign of 1/d (BVH4
-// nodes: the selection is an address offset, no per-plane selects); same values as
-// slab().
+// Conservative slab test on a padded box (PBRT-style 1+2*gamma3 on t_far).
+// t = (lo - o) / d is evaluated as fma(lo, 1/d, -o/d): pruning only, so the few-ulp
+// error of the estimate is covered by the box padding (~1e-6 of the scene scale,
+// >> |o/d| ulp) and the 1+2*gamma3 factor on t_far.  The near and far plane of each
+// axis are chosen by the sign of 1/d, NOT by min/max of the two distances: for a
+// direction component of exactly 0 (1/d = inf) a plane distance can be NaN, and
+// fminf/fmaxf would then turn the other plane's -inf into the FAR distance and cull
+// a box the ray lies inside (measured: 8 of 262144 pixels at config 2).  With the
+// selection, a NaN distance is dropped by the fmaxf/fminf that follow, which can
+// only enlarge the interval.  For f32 BVH4 nodes the selection is an address offset
+// (no per-plane selects); quantised nodes swap their plane words (qchild).
 __device__ __forceinline__ bool slab_nf(float nx, float fx, float ny, float fy, float nz, float fz, V3 oi, V3 inv,
                                         float tmin, float tmax, float& tn) {
     float ax = __builtin_fmaf(nx, inv.x, -oi.x), bx = __builtin_fmaf(fx, inv.x, -oi.x);
@@ -609,7 +384,8 @@ template <bool STATS, int MODE, class S, bool QN = false, bool RES = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
                                              float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0,
-                                             int* fault = nullptr, int leaf_break = 0, int leaf_exit = 0) {
+                                             int* fault = nullptr, int leaf_break = 0, int leaf_exit = 0,
+                                             uint32_t guard_lim = kGuardTrips) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
     V3 oi = o * inv;
@@ -720,7 +496,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
         if (RES && (cur != kSentinel || leaf < 0) && __popcll(__ballot(true)) < min_lanes) break;
         // watchdog: a traversal revisiting nodes forever (corrupt tree) ends the query and
         // raises the fault flag that the host turns into an error, instead of hanging the GPU
-        if (++guard > kGuardTrips) {
+        if (++guard > guard_lim) {
             if (fault) atomicOr(fault, 1);
             cur = kSentinel;
             leaf = 0;
@@ -823,9 +599,9 @@ __device__ __forceinline__ float area_light_pdf(float t_light, V3 dir, V3 light_
 template <int STACK, bool STATS, int VAR, bool SCENE_LDS, int WPE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel(TraceParams P) {
-    // VAR = traversal kind (0 split, 1 unified, 2 while-while BVH2, 3 while-while BVH4,
-    // 4 BVH4 + parked state) | 8 for phase-aligned scheduling (see below)
-    constexpr int TRAV = VAR & 7;
+    // VAR bits: 8 phase-aligned scheduling (see below), 32 spill stack, 64 quantised
+    // nodes, 128 suspended traversal tails, 256 MIS direct lighting; the traversal is
+    // always the while-while BVH4 (traverse_ww4)
     constexpr bool PHASE = (VAR & 8) != 0;
     constexpr bool SPILL = (VAR & 32) != 0;    // LDS stack of STACK entries + global spill area
     constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
@@ -833,9 +609,6 @@ void trace_kernel(TraceParams P) {
     constexpr bool MIS = (VAR & 256) != 0;     // MIS direct lighting (sample_direct_lighting2) instead of NEE
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
-    // VAR 4: BVH4 traversal with the path state (beta, L, pend, wi) parked in LDS
-    // while the lane traverses, so traversal registers do not add to it.
-    constexpr int kParkF4 = (TRAV == 4) ? 3 * kBlock : 0;
     int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
     using StackT = typename std::conditional<SPILL, SpillStack<STACK>, LdsStack>::type;
     StackT stk;
@@ -844,7 +617,6 @@ void trace_kernel(TraceParams P) {
         stk.g = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
         stk.gs = gridDim.x * kBlock;
     }
-    float4* park = smem + kStackWords * kBlock / 4 + threadIdx.x;
     const float4* g_nodes = P.nodes;
     const float4* g_tris = P.tris;
     const float4* s_nm = P.tri_nm;
@@ -855,7 +627,7 @@ void trace_kernel(TraceParams P) {
     if (SCENE_LDS) {
         // small scene: copy BVH + triangles, and the shading data (normals, frames,
         // materials, emitters), into LDS once per persistent block
-        float4* sn = smem + kStackWords * kBlock / 4 + kParkF4;
+        float4* sn = smem + kStackWords * kBlock / 4;
         float4* st4 = sn + P.n_node_f4;
         float4* snm = st4 + P.n_tri_f4;
         float4* sfr = snm + P.n_tri;
@@ -1013,14 +785,8 @@ void trace_kernel(TraceParams P) {
         // the leaf-phase entry / exit thresholds (counts of lanes) are tuned for full waves; in
         // the drain, with few lanes left, they would switch phase after every trip
         const int lb = exhausted ? 0 : P.leaf_break, le = exhausted ? 0 : P.leaf_exit;
-        if (TRAV == 0) {
-            if (qtype == Q_EXT) hit = traverse<false, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
-            else hit = traverse<true, STATS>(P, o, d, kTMin, tmax, lstack, hid, ht, cn);
-        } else if (TRAV == 1) {
-            hit = traverse_u<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
-        } else if (TRAV == 2) {
-            hit = traverse_ww<STATS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, lstack, hid, ht, cn);
-        } else if (TRAV == 3 && RESUME) {
+        const uint32_t glim = P.guard_trips;
+        if (RESUME) {
             if (!pending) tstate_init(tst, stk, tmax);
             // suspending a query only pays while idle lanes can be refilled: once the work
             // queue is exhausted (the launch's drain) the wave keeps traversing instead of
@@ -1028,34 +794,28 @@ void trace_kernel(TraceParams P) {
             const int res_min = exhausted ? 0 : P.resume_min;
             bool done;
             if (PHASE && do_shadow)
-                done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn,
-                                                                  &tst, res_min, P.fault, lb, le);
+                done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
             else if (PHASE)
-                done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht,
-                                                                  cn, &tst, res_min, P.fault, lb, le);
+                done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
             else
-                done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk,
-                                                                  hid, ht, cn, &tst, res_min, P.fault, lb, le);
+                done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax,
+                                                                  qtype == Q_SHADOW, stk, hid, ht, cn, &tst, res_min,
+                                                                  P.fault, lb, le, glim);
             pending = !done;
             if (pending) continue;   // resume next iteration; no shading yet
             hit = hid >= 0;
-        } else if (TRAV == 3 && PHASE) {
-            if (do_shadow) hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
-            else hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
-        } else if (TRAV == 3) {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
+        } else if (PHASE) {
+            if (do_shadow)
+                hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
+            else
+                hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
         } else {
-            park[0] = make_float4(beta.x, beta.y, beta.z, L.x);
-            park[kBlock] = make_float4(L.y, L.z, pend.x, pend.y);
-            park[2 * kBlock] = make_float4(pend.z, wi.x, wi.y, wi.z);
-            asm volatile("" ::: "memory");
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, stk, hid, ht, cn, nullptr, 0, P.fault, lb, le);
-            asm volatile("" ::: "memory");
-            float4 k0 = park[0], k1 = park[kBlock], k2 = park[2 * kBlock];
-            beta = v3(k0.x, k0.y, k0.z);
-            L = v3(k0.w, k1.x, k1.y);
-            pend = v3(k1.z, k1.w, k2.x);
-            wi = v3(k2.y, k2.z, k2.w);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
+                                                              stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim);
         }
 
         if (P.n_sph > 0 && !(qtype == Q_SHADOW && hit)) {
@@ -1349,41 +1109,13 @@ void trace_kernel(TraceParams P) {
 
 }  // namespace
 
-// variant table: (traversal | 8 phase-aligned, LDS scene, min waves per SIMD); see prt_kernels.h
-#define PRT_VARIANTS(X)                                   \
-    X(kVarSplit, 0, false, 1)                             \
-    X(kVarUnified, 1, false, 1)                           \
-    X(kVarUnifiedLds, 1, true, 1)                         \
-    X(kVarWW, 2, false, 1)                                \
-    X(kVarWWLds, 2, true, 1)                              \
-    X(kVarWWLds5, 2, true, 5)                             \
-    X(kVarWWLds6, 2, true, 6)                             \
-    X(kVarWW5, 2, false, 5)                               \
-    X(kVarWW4, 3, false, 1)                               \
-    X(kVarWW4Lds, 3, true, 1)                             \
-    X(kVarWW4Lds6, 3, true, 6)                            \
-    X(kVarWW4ParkLds6, 4, true, 6)                        \
-    X(kVarWW4ParkLds7, 4, true, 7)                        \
-    X(kVarWW4Park5, 4, false, 5)                        \
-    X(kVarWW4PhLds6, 11, true, 6)                        \
-    X(kVarWW4PhLds, 11, true, 1)                         \
-    X(kVarWW4Ph, 11, false, 1)                           \
-    X(kVarWW4Ph5, 11, false, 5)                          \
-    X(kVarWW4Sp, 35, false, 1)                           \
-    X(kVarWW4Sp4, 35, false, 4)                          \
-    X(kVarWW4Sp5, 35, false, 5)                          \
-    X(kVarWW4QSp, 99, false, 1)                          \
-    X(kVarWW4QSp5, 99, false, 5)                         \
-    X(kVarWW4QPhSp, 107, false, 1)                       \
-    X(kVarWW4QSp6, 99, false, 6)                         \
-    X(kVarWW4PhRLds6, 139, true, 6)                      \
-    X(kVarWW4RLds6, 131, true, 6)                        \
-    X(kVarWW4QRSp5, 227, false, 5)                       \
-    X(kVarWW4PhLds7, 11, true, 7)                        \
-    X(kVarWW4PhLds5, 11, true, 5)                        \
-    X(kVarWW4QRSp6, 227, false, 6)                       \
-    X(kVarWW4Lds6Mis, 259, true, 6)                      \
-    X(kVarWW4QRSp6Mis, 483, false, 6)
+// variant table: (VAR bits of trace_kernel, LDS-resident scene, min waves per SIMD); see prt_kernels.h
+#define PRT_VARIANTS(X)                       \
+    X(kVarLds, 8, true, 6)                    \
+    X(kVarLdsAnyOcc, 8, true, 1)              \
+    X(kVarGlobal, 224, false, 6)              \
+    X(kVarLdsMis, 256, true, 6)               \
+    X(kVarGlobalMis, 480, false, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
@@ -1400,8 +1132,8 @@ static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStr
 template <int STACK, bool STATS>
 static hipError_t launch_var(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream) {
     switch (var) {
-#define X(id, trav, lds, wpe) \
-        case id: return launch_one<STACK, STATS, trav, lds, wpe>(P, grid, smem, stream);
+#define X(id, bits, lds, wpe) \
+        case id: return launch_one<STACK, STATS, bits, lds, wpe>(P, grid, smem, stream);
         PRT_VARIANTS(X)
 #undef X
         default: return hipErrorInvalidValue;
@@ -1419,8 +1151,8 @@ template <int STACK, bool STATS>
 static int occ_var(int var, size_t smem) {
     int n = 0;
     switch (var) {
-#define X(id, trav, lds, wpe) \
-        case id: occ_one<STACK, STATS, trav, lds, wpe>(&n, smem); break;
+#define X(id, bits, lds, wpe) \
+        case id: occ_one<STACK, STATS, bits, lds, wpe>(&n, smem); break;
         PRT_VARIANTS(X)
 #undef X
         default: break;

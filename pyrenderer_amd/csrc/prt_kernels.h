@@ -21,7 +21,8 @@ struct TraceParams {
     // the ray origin M (0,0,0,1) and the constant terms rd.z * M[i][2] of gen_ray,
     // evaluated on the host in the kernel's f32 order (camera_taichi.py:47-74)
     int cam_fast;
-    int* fault;               // watchdog flag (non-zero: a traversal exceeded kGuardTrips)
+    int* fault;               // watchdog flag (non-zero: a traversal exceeded guard_trips)
+    uint32_t guard_trips;     // traversal phases per query before the watchdog trips (env PRT_GUARD_TRIPS)
     int leaf_break;           // while-while: enter the leaf phase when <= this many descending lanes lack a leaf
     int leaf_exit;            // ... and leave it when <= this many lanes still hold a leaf
     int resume_min;           // resume variants: leave the traversal loop below this many active lanes
@@ -48,47 +49,22 @@ struct TraceParams {
     const int* sph_mat;
 };
 
-// trace kernel variants (A/B-able at run time through PRT_FLAG_VARIANT)
-constexpr int kVarSplit = 1;       // separate closest-hit / any-hit traversal calls (round-1 baseline)
-constexpr int kVarUnified = 2;     // one traversal loop for both query kinds
-constexpr int kVarUnifiedLds = 3;  // unified + BVH/triangles copied into LDS (small scenes)
-constexpr int kVarWW = 4;          // while-while traversal (Aila-Laine), global scene
-constexpr int kVarWWLds = 5;       // while-while + LDS-resident scene
-constexpr int kVarWWLds5 = 6;      // ... compiled for >= 5 waves per SIMD
-constexpr int kVarWWLds6 = 7;      // ... compiled for >= 6 waves per SIMD
-constexpr int kVarWW5 = 8;         // while-while, global scene, >= 5 waves per SIMD
-constexpr int kVarWW4 = 9;         // while-while over the BVH4, global scene
-constexpr int kVarWW4Lds = 10;     // ... LDS-resident scene
-constexpr int kVarWW4Lds6 = 11;    // ... LDS-resident scene, >= 6 waves per SIMD
-constexpr int kVarWW4ParkLds6 = 12; // BVH4 + path state parked in LDS during traversal, LDS scene, >= 6 waves
-constexpr int kVarWW4ParkLds7 = 13; // ... >= 7 waves
-constexpr int kVarWW4Park5 = 14;    // BVH4 + parked state, global scene, >= 5 waves
-constexpr int kVarWW4PhLds6 = 15;   // BVH4, LDS scene, >= 6 waves, phase-aligned ext/shadow iterations
-constexpr int kVarWW4PhLds = 16;    // ... LDS scene, no occupancy target
-constexpr int kVarWW4Ph = 17;       // ... global scene
-constexpr int kVarWW4Ph5 = 18;      // ... global scene, >= 5 waves
-constexpr int kVarWW4Sp = 19;       // BVH4, global scene, 32-entry LDS stack + global spill area
-constexpr int kVarWW4Sp4 = 20;      // ... >= 4 waves per SIMD
-constexpr int kVarWW4Sp5 = 21;      // ... >= 5 waves per SIMD
-constexpr int kVarWW4QSp = 22;      // quantised 64-B BVH4 nodes, spill stack, global scene
-constexpr int kVarWW4QSp5 = 23;     // ... >= 5 waves per SIMD
-constexpr int kVarWW4QPhSp = 24;    // ... phase-aligned
-constexpr int kVarWW4QSp6 = 25;     // ... >= 6 waves per SIMD
-constexpr int kVarWW4PhRLds6 = 26;  // phase-aligned + suspended traversal tails (resume), LDS scene, >= 6 waves
-constexpr int kVarWW4RLds6 = 27;    // resume, mixed schedule, LDS scene, >= 6 waves
-constexpr int kVarWW4QRSp5 = 28;    // resume, quantised nodes, spill stack, >= 5 waves
-constexpr int kVarWW4PhLds7 = 29;   // phase-aligned, LDS scene, >= 7 waves per SIMD
-constexpr int kVarWW4PhLds5 = 30;   // ... >= 5 waves per SIMD
-constexpr int kVarWW4QRSp6 = 31;   // resume, quantised nodes, spill stack, >= 6 waves per SIMD
+// trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the
+// while-while BVH4 traversal (prt_device.h traverse_ww4) and give bit-identical images;
+// the measured history of the variants this set replaced is in DESIGN.md §2.
+constexpr int kVarLds = 1;         // LDS-resident scene, phase-aligned ext/shadow iterations, >= 6 waves/SIMD
+constexpr int kVarLdsAnyOcc = 2;   // ... no occupancy target (LDS scenes too large for 6 blocks per CU)
+constexpr int kVarGlobal = 3;      // global scene: quantised 64-B nodes, LDS stack + global spill area,
+                                   // suspended traversal tails, >= 6 waves/SIMD
 // estimator variants: the reference's unused MIS direct lighting (PRT_FLAG_MIS_NEE)
-constexpr int kVarWW4Lds6Mis = 32;   // kVarWW4Lds6 + MIS, LDS scene
-constexpr int kVarWW4QRSp6Mis = 33;  // kVarWW4QRSp6 + MIS, global scene
-constexpr int kVarLast = 33;
+constexpr int kVarLdsMis = 4;      // LDS scene, mixed schedule, >= 6 waves/SIMD
+constexpr int kVarGlobalMis = 5;   // kVarGlobal + MIS
+constexpr int kVarFirst = 1;
+constexpr int kVarLast = 5;
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
 bool variant_quantized(int var);
-bool variant_uses_bvh4(int var);
 
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float
     int hid = -1;
     float ht = 0.0f;
     bool hit = traverse_ww4<false, ANY ? 2 : 1, LdsStack, QN>(P.nodes, P.tris, o, d, a.w, b.w, ANY, stk, hid, ht, cn,
-                                                              nullptr, 0, P.fault);
+                                                              nullptr, 0, P.fault, 0, 0, P.guard_trips);
     if (P.n_sph > 0 && !(ANY && hit)) {
         float best = hit ? ht : b.w;
         for (int k = 0; k < P.n_sph; ++k) {
@@ -122,19 +122,8 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
 
 }  // namespace
 
-bool variant_uses_lds(int var);
-
 // entries needed: one per level (<= depth) plus the while-while sentinel
 int stack_variant(int depth) { return depth + 1 <= 10 ? 10 : depth + 1 <= 16 ? 16 : depth + 1 <= 32 ? 32 : 64; }
-
-static bool variant_parks(int var) {
-    switch (var) {
-#define X(id, trav, lds, wpe) case id: return (trav & 7) == 4;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
 
 size_t lds_scene_bytes(const TraceParams& P) {
     return 16 * ((size_t)P.n_node_f4 + P.n_tri_f4 + 7 * (size_t)P.n_tri + 2 * (size_t)P.n_mat + 4 * (size_t)P.n_lt) +
@@ -143,7 +132,6 @@ size_t lds_scene_bytes(const TraceParams& P) {
 
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
     size_t b = (size_t)stack * kBlock * sizeof(int);
-    if (variant_parks(var)) b += 48 * (size_t)kBlock;
     if (variant_uses_lds(var)) b += lds_scene_bytes(P);
     return b;
 }
@@ -194,18 +182,9 @@ hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, b
     return hipGetLastError();
 }
 
-bool variant_uses_bvh4(int var) {
-    switch (var) {
-#define X(id, trav, lds, wpe) case id: return (trav & 7) >= 3;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
-
 bool variant_mis(int var) {
     switch (var) {
-#define X(id, trav, lds, wpe) case id: return (trav & 256) != 0;
+#define X(id, bits, lds, wpe) case id: return (bits & 256) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;
@@ -214,7 +193,7 @@ bool variant_mis(int var) {
 
 bool variant_quantized(int var) {
     switch (var) {
-#define X(id, trav, lds, wpe) case id: return (trav & 64) != 0;
+#define X(id, bits, lds, wpe) case id: return (bits & 64) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;
@@ -223,7 +202,7 @@ bool variant_quantized(int var) {
 
 bool variant_spills(int var) {
     switch (var) {
-#define X(id, trav, lds, wpe) case id: return (trav & 32) != 0;
+#define X(id, bits, lds, wpe) case id: return (bits & 32) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;
@@ -232,7 +211,7 @@ bool variant_spills(int var) {
 
 bool variant_uses_lds(int var) {
     switch (var) {
-#define X(id, trav, lds, wpe) case id: return lds;
+#define X(id, bits, lds, wpe) case id: return lds;
         PRT_VARIANTS(X)
 #undef X
         default: return false;

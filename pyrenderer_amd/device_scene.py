@@ -163,6 +163,12 @@ class DeviceScene:
         N.check(N.lib().prt_kernel_timing(self.h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def check_faults(self):
+        """Synchronise the device and raise PrtError if the traversal watchdog tripped in the
+        last render of any of this scene's streams (device-output renders are not checked
+        otherwise)."""
+        N.check(N.lib().prt_check_faults(self.h))
+
     def last_stats(self):
         s = np.zeros(4, np.uint64)
         N.check(N.lib().prt_last_stats(self.h, N.ptr(s)))

@@ -17,9 +17,12 @@ from .device_scene import interleaved_tiles, max_tiles_per_rank, tile_grid, unpa
 
 
 class TileShard:
-    """This rank's tiles and the padded gather buffers (allocated once)."""
+    """This rank's tiles and the padded gather buffers (allocated once).
 
-    def __init__(self, W, H, tile, rank, world, device, scheme="latin"):
+    `buf` holds the rank's per-tile radiance sums on `device`.  With `host_staging` (the
+    gloo backend, which moves CPU tensors) gather() first copies them to host memory."""
+
+    def __init__(self, W, H, tile, rank, world, device, scheme="latin", host_staging=False):
         self.W, self.H, self.tile, self.rank, self.world = W, H, tile, rank, world
         self.scheme = scheme
         tx, ty = tile_grid(W, H, tile)
@@ -28,13 +31,18 @@ class TileShard:
         self.max_tiles = max_tiles_per_rank(W, H, tile, world, scheme)
         self.slot_elems = tile * tile * 3
         self.buf = torch.zeros(self.max_tiles * self.slot_elems, dtype=torch.float32, device=device)
-        self.gather_list = ([torch.empty_like(self.buf) for _ in range(world)]
+        self.host_staging = bool(host_staging) and self.buf.is_cuda
+        self.wire = torch.empty_like(self.buf, device="cpu") if self.host_staging else self.buf
+        self.gather_list = ([torch.empty_like(self.wire) for _ in range(world)]
                             if (world > 1 and rank == 0) else None)
 
     def gather(self, group=None):
-        """Collective: rank 0 receives every rank's tile sums (no-op for world 1)."""
+        """Collective: rank 0 receives every rank's tile sums (no-op for world 1).  Runs on
+        torch's current stream: callers that rendered on another stream enter it first."""
         if self.world > 1:
-            dist.gather(self.buf, self.gather_list, dst=0, group=group)
+            if self.host_staging:
+                self.wire.copy_(self.buf)       # synchronous device-to-host copy on the current stream
+            dist.gather(self.wire, self.gather_list, dst=0, group=group)
 
     def assemble(self):
         """Rank 0: (W, H, 3) float32 sums frame from the gathered buffers."""
@@ -48,16 +56,39 @@ class TileShard:
 
 
 def render_distributed(device_scene, cam_packed, W, H, spp, depth, seed=0, tile=64, group=None, stream=None):
-    """Render a frame across the ranks of the default group; returns mean radiance
-    (W, H, 3) on rank 0 and None elsewhere."""
-    rank = dist.get_rank() if dist.is_initialized() else 0
-    world = dist.get_world_size() if dist.is_initialized() else 1
+    """Render a frame across the ranks of `group` (default: the default group); returns mean
+    radiance (W, H, 3) on rank 0 and None elsewhere.
+
+    The render and the gather are ordered on `stream` (default: torch's current stream of the
+    scene's device).  Before the gather every rank synchronises and reads its traversal
+    watchdog (prt_check_faults); the flags are combined with a MAX all-reduce, so a fault on
+    any rank raises PrtError on every rank instead of returning a silently invalid frame."""
+    from ._native import PRT_ERR_INTERNAL, PrtError
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
     dev = torch.device("cuda", device_scene.device)
-    shard = TileShard(W, H, tile, rank, world, dev)
+    host = world > 1 and dist.get_backend(group) == "gloo"
+    shard = TileShard(W, H, tile, rank, world, dev, host_staging=host)
     s = stream or torch.cuda.current_stream(dev)
     device_scene.render_tiles_device(cam_packed, W, H, tile, tile, shard.tiles, spp, depth, shard.buf.data_ptr(),
                                      s.cuda_stream, seed=seed)
-    shard.gather(group)
+    try:
+        device_scene.check_faults()
+        fault = 0
+    except PrtError as e:
+        if e.code != PRT_ERR_INTERNAL:
+            raise
+        fault = 1
+    if world > 1:
+        f = torch.tensor([fault], dtype=torch.int32, device="cpu" if host else dev)
+        with torch.cuda.stream(s):
+            dist.all_reduce(f, op=dist.ReduceOp.MAX, group=group)
+        fault = int(f.item())
+    if fault:
+        raise PrtError(PRT_ERR_INTERNAL, "traversal watchdog tripped on "
+                       + ("this rank" if world == 1 else "at least one rank") + "; the frame is invalid")
+    with torch.cuda.stream(s):
+        shard.gather(group)
     if rank != 0:
         return None
     torch.cuda.synchronize(dev)

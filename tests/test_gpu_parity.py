@@ -74,7 +74,7 @@ def test_tiling_and_sharding_invariance(gpu_scene, cornell):
     assert not np.array_equal(_gpu_frame(gpu_scene, cam, 96, 80, 4, 8, seed=6), a)
 
 
-def test_edge_cases(gpu_scene, cornell):
+def test_edge_cases(gpu_scene, oracle_scene, cornell):
     cam = cornell[1].convert_to_taichi_camera().packed()
     z, _ = gpu_scene.render_tiles(cam, 8, 8, 8, 8, np.array([0], np.int32), 0, 8)
     assert not z.any()
@@ -83,8 +83,8 @@ def test_edge_cases(gpu_scene, cornell):
     e, _ = gpu_scene.render_tiles(cam, 8, 8, 8, 8, np.zeros(0, np.int32), 4, 4)
     assert e.shape == (0, 3)
     t, _ = gpu_scene.render_tiles(cam, 2, 2, 8, 8, np.array([0], np.int32), 2, 3)
-    t = t.reshape(8, 8, 3)
-    assert t[:2, :2].any() or True
+    t = t.reshape(8, 8, 3)                              # [ly][lx]
+    np.testing.assert_array_equal(t[:2, :2].transpose(1, 0, 2), oracle_scene.render(cam, 2, 2, 2, 3, seed=0))
     assert not t[2:].any() and not t[:, 2:].any()       # outside the 2x2 frame stays 0
     from pyrenderer_amd._native import PrtError
     with pytest.raises(PrtError):
@@ -183,8 +183,9 @@ def test_specular_scene_matches_oracle(rough):
 
 
 def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
-    """Every trace-kernel variant (split / unified / while-while, BVH2 / BVH4,
-    global / LDS scene, occupancy targets) renders the same bits as the oracle."""
+    """Every trace-kernel variant of the reference estimator (LDS scene with and without the
+    occupancy target, global scene: quantised nodes, spill stack, suspended tails) renders
+    the same bits as the oracle."""
     from pyrenderer_amd.device_scene import interleaved_tiles
     cam = cornell[1].convert_to_taichi_camera().packed()
     ids = interleaved_tiles(64, 64, 32)
@@ -209,7 +210,7 @@ def test_frames_in_flight_on_two_streams(gpu_scene, oracle_scene, cornell):
     streams = [torch.cuda.Stream(dev) for _ in range(2)]
     outs = [torch.empty(len(ids) * tile * tile * 3, dtype=torch.float32, device=dev) for _ in range(4)]
     for k in range(4):
-        v = (N.VAR_WW4_PH_LDS6 if k % 2 else 0) << 8
+        v = (N.VAR_GLOBAL if k % 2 else 0) << 8
         gpu_scene.render_tiles_device(cam, W, W, tile, tile, ids, spp, 8, outs[k].data_ptr(),
                                       streams[k % 2].cuda_stream, seed=7, flags=v)
     torch.cuda.synchronize(dev)
@@ -276,7 +277,7 @@ def test_general_camera_matches_oracle(gpu_scene, oracle_scene, cornell, mod):
 
 
 def test_spill_stack_matches_oracle(cornell, oracle_scene, monkeypatch):
-    """Spill variants with a 4-entry LDS stack (PRT_SPILL_LDS=4): the Cornell box's
+    """The global-scene kernel with a 4-entry LDS stack (PRT_SPILL_LDS=4): the Cornell box's
     traversal stack reaches 8 entries, so the global spill area is exercised."""
     from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
     monkeypatch.setenv("PRT_SPILL_LDS", "4")
@@ -284,9 +285,9 @@ def test_spill_stack_matches_oracle(cornell, oracle_scene, monkeypatch):
     cam = cornell[1].convert_to_taichi_camera().packed()
     ids = interleaved_tiles(64, 64, 32)
     o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
-    for v in (19, 20, 21):
-        g, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
-        assert np.array_equal(g, o), v
+    from pyrenderer_amd import _native as N
+    g, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, N.VAR_GLOBAL << 8)
+    assert np.array_equal(g, o)
 
 
 def test_large_frame_matches_oracle(gpu_scene, oracle_scene, cornell):
@@ -330,7 +331,9 @@ def test_mis_direct_lighting_variant_matches_oracle(gpu_scene, oracle_scene, cor
     with pytest.raises(N.PrtError):
         gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, N.VAR_MIS[0] << 8)
     with pytest.raises(N.PrtError):
-        gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, N.PRT_FLAG_MIS_NEE | (15 << 8))
+        gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, N.PRT_FLAG_MIS_NEE | (N.VAR_LDS << 8))
+    with pytest.raises(N.PrtError):
+        gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, (N.VAR_MIS[1] + 1) << 8)   # unknown id
 
 
 def test_mis_variant_on_a_global_scene_matches_oracle(cornell):

@@ -69,7 +69,7 @@ def test_gpu_matches_oracle_with_three_lights(multi):
     g, _ = ds.render_tiles(cam, 96, 64, 32, 32, ids, 4, 8, 8)
     np.testing.assert_array_equal(g, o)
     # the global-scene kernel and the MIS estimator over the same lights
-    g2, _ = ds.render_tiles(cam, 96, 64, 32, 32, ids, 4, 8, 8, N.VAR_WW4_Q_SP5 << 8)
+    g2, _ = ds.render_tiles(cam, 96, 64, 32, 32, ids, 4, 8, 8, N.VAR_GLOBAL << 8)
     np.testing.assert_array_equal(g2, o)
     O.set_nee_mode(True)
     try:
