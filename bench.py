@@ -37,14 +37,19 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 LDS_PEAK_GBS = 150000.0  # MI355X_MICROARCH.md §LDS: ~150 TB/s aggregate for ds_read_b128 at ~2.4 GHz
 VALU_PEAK_TFLOPS = 157.3
-# Algorithmic bytes per unit of work: one BVH node record
-# (two child boxes + refs), one triangle record (v0, e1, e2 + id), one light
-# triangle record per shadow query, the per-sample radiance write + its reduction
-# re-read, and the final per-pixel sum write.
-# A node visit reads its child boxes: 64 B for a BVH2 node (2 boxes + refs), 112 B
-# for a BVH4 node (4 boxes SoA + refs); bench picks the figure of the kernel in use.
-# (64 B for a quantised BVH4 node, the layout used for scenes that do not fit LDS).
-B_NODE2, B_NODE4, B_NODE4Q, B_TRI, B_LIGHT, B_SAMPLE, B_PIXEL = 64, 112, 64, 48, 64, 24, 12
+SIMDS, PEAK_CLOCK_GHZ = 1024, 2.4   # 256 CUs x 4 SIMD-32; a wave64 VALU instruction holds its SIMD 2 cycles
+# Algorithmic bytes per sample, SURVEY.md §8(d) (the roofline's `achieved`):
+#   B_sample = 32 N_node + 48 N_tri + 48 N_lightpt + 16 N_ray + 12 / spp_per_launch
+# N_node = BVH node visits (one BVH4 visit counted as one 32-B node fetch, as §8(d)'s
+# per-visit figure; the BVH4 visits replace ~2-3 BVH2 visits each, so this is the
+# conservative side), N_tri = triangle tests, N_lightpt = NEE light samples that issue a
+# shadow query, N_ray = 0 (one persistent kernel: no ray state passes between stages),
+# 12 B per pixel = the framebuffer write.
+S8_NODE, S8_TRI, S8_LIGHT, S8_PIXEL = 32, 48, 48, 12
+# Logical bytes the kernel actually reads per unit (the `lds` block for LDS-resident scenes):
+# 112 B per f32 BVH4 node (4 boxes SoA + refs), 64 B per quantised node, 48 B per triangle,
+# 64 B per light record.
+B_NODE4, B_NODE4Q, B_TRI, B_LIGHT = 112, 64, 48, 64
 # f32 operation accounting (no FMA under the parity contract): slab test of one
 # child box ~ 20 ops, Moller-Trumbore ~ 45 ops (with the division).
 F_BOX, F_TRI = 20, 45
@@ -115,6 +120,25 @@ def load_scene(name):
     raise SystemExit(f"unknown scene {name}")
 
 
+def host_cpu():
+    """(threads used, affinity cores, CPU model): the CPU legs use every core this process
+    may run on, capped by OMP_NUM_THREADS when the environment sets it (the GPU box sets it to
+    the box's CPU share, 16 per GPU, while its affinity mask shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "").strip()
+    threads = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return threads, aff, model
+
+
 def cpu_sample(flat, cam, args, seconds):
     """Oracle (C restatement of PathTracer.trace, OpenMP) on a bounded sample of the
     same workload: random 8x8 tiles of the frame at the full spp/depth, sized to about
@@ -126,7 +150,7 @@ def cpu_sample(flat, cam, args, seconds):
     osc = O.OracleScene.from_flat(flat)
     nodes, _, order = Bvh(flat.tri_v).export()
     osc.set_bvh(nodes, order)
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    cores = host_cpu()[0]
     W = H = args.res
     n_tiles_total = (W // 8) * (H // 8)
     rng = np.random.default_rng(1)
@@ -149,19 +173,22 @@ def cpu_baseline(ids, dt, cores, args):
     W = H = args.res
     n = len(ids)
     samples = n * 64 * args.spp
+    _, aff, model = host_cpu()
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "cpu_model": model, "affinity_cores": aff,
             "sample": f"{n} random 8x8 tiles of the {W}x{H} frame at {args.spp} spp, depth {args.depth} "
                       f"({samples} samples, {dt:.1f} s); oracle/prt_oracle.c (C port of PathTracer.trace), "
                       f"BVH2 closest hit, OpenMP {cores} threads"}
 
 
-def numpy_baseline(flat, cam, args, seconds):
+def numpy_baseline(flat, cam, args, seconds, procs=None):
     """main.py's NumPy path counterpart (oracle/numpy_path.py: PathTracer.trace as array code
     over ray batches, bit-identical to the C oracle), one spawned process per core like
-    main.py's joblib workers, on random 8x8 tiles sized to ~`seconds`.  Returns (report,
-    tile ids, sums) or (note, None, None) for scenes outside its scope (config 3, 4)."""
+    main.py's joblib workers (or `procs` of them: main.py:52 itself uses n_jobs=4), on random
+    8x8 tiles sized to ~`seconds`.  Returns (report, tile ids, sums) or (note, None, None) for
+    scenes outside its scope (config 3, 4)."""
     from oracle import numpy_path as NP
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    cores = procs or host_cpu()[0]
     W = H = args.res
     try:
         ids, sums, dt = NP.timed_sample(flat, cam, W, H, args.spp, args.depth, args.seed, seconds, cores)
@@ -288,23 +315,33 @@ def main():
         kinfo = ds.kernel_info()
         if args.variant:
             kinfo = dict(kinfo, variant=args.variant)
-        arity = kinfo["bvh_arity"]
-        b_node = (B_NODE4Q if kinfo["quantized"] else B_NODE4) if arity == 4 else B_NODE2
-        bytes_launch = ((b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank
-                        + B_SAMPLE * n_px_rank * args.spp + B_PIXEL * n_px_rank) / launches_per_step
-        achieved = bytes_launch / (kern_avg_ms * 1e-3) / 1e9
-        # the scene part of those bytes (nodes, triangles, light records): LDS reads for an
-        # LDS-resident scene
-        scene_gbs = ((b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * per_rank / launches_per_step
-                     / (kern_avg_ms * 1e-3) / 1e9)
-        flops_launch = (F_BOX * arity * nodes + F_TRI * tris) * per_rank / launches_per_step
-        traffic, pmc = None, {}
+        # SURVEY.md §8(d) algorithmic bytes per launch (module constants S8_*)
+        work_launch = per_rank / launches_per_step
+        bytes_launch = (S8_NODE * nodes + S8_TRI * tris + S8_LIGHT * shadow) * work_launch + S8_PIXEL * n_px_rank
+        kern_s = kern_avg_ms * 1e-3
+        achieved = bytes_launch / kern_s / 1e9
+        # what the kernel really reads per launch from its scene copy (LDS for LDS-resident scenes)
+        b_node = B_NODE4Q if kinfo["quantized"] else B_NODE4
+        scene_gbs = (b_node * nodes + B_TRI * tris + B_LIGHT * shadow) * work_launch / kern_s / 1e9
+        flops_launch = (F_BOX * 4 * nodes + F_TRI * tris) * work_launch
+        # counter figures (PMC passes, tools/profile_bench.sh -> tools/pmc_summary.py) only when
+        # they were measured on this exact kernel build and variant
+        from pyrenderer_amd.build import kernel_sha
+        sha = kernel_sha()
+        pmc, pmc_state = {}, "no entry"
         if args.pmc_json and os.path.exists(args.pmc_json) and world == 1:
             try:
-                pmc = json.load(open(args.pmc_json)).get(f"{args.scene}_{W}x{H}x{args.spp}spp_d{args.depth}", {})
+                e = json.load(open(args.pmc_json)).get(f"{args.scene}_{W}x{H}x{args.spp}spp_d{args.depth}")
             except (OSError, ValueError):
-                pmc = {}
-            traffic = pmc.get("hbm_bytes_per_launch")
+                e = None
+            if e:
+                if e.get("kernel_sha") == sha and e.get("variant") == kinfo["variant"]:
+                    pmc, pmc_state = e, "this build"
+                else:
+                    pmc_state = f"stale (measured on kernel {e.get('kernel_sha')} variant {e.get('variant')})"
+        traffic = pmc.get("hbm_bytes_per_launch")
+        issue = pmc.get("valu_issue_util")
+        lane = pmc.get("valu_lane_util")
         cpu, l2, cpu_np = None, None, None
         if not args.no_cpu_baseline and world == 1 and args.numpy_seconds > 0:
             cpu_np, np_ids, np_sums = numpy_baseline(flat, cam, args, args.numpy_seconds)
@@ -312,6 +349,9 @@ def main():
                 torch.cuda.synchronize(dev)
                 cmp = l2_vs_cpu(shards[0].assemble(), np_ids, np_sums, args)
                 cpu_np["l2_vs_gpu"] = {k: cmp[k] for k in ("pixels", "rmse", "max_pixel_l2", "identical_pixels")}
+                # main.py:52's own parallelism (joblib n_jobs=4), on a shorter sample
+                n4, _, _ = numpy_baseline(flat, cam, args, args.numpy_seconds / 2, procs=4)
+                cpu_np["n_jobs_4"] = {k: n4.get(k) for k in ("value", "cores", "sample")}
         if not args.no_cpu_baseline:
             # at N = 1 the baseline sample (~cpu_seconds) doubles as the accuracy sample; at
             # N > 1 only a short accuracy sample of the gathered frame is rendered on the CPU
@@ -330,21 +370,26 @@ def main():
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
                        "tile_scheme": args.scheme, "frames_in_flight": n_streams,
                        "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "hbm_measured_frac": (round(traffic / kern_s / 1e9 / HBM_PEAK_GBS, 4)
+                                               if traffic else None),
+                         "valu_issue_util": issue, "valu_lane_util": lane,
                          "kernel": "trace_kernel", "kernel_avg_ms": round(kern_avg_ms, 4),
-                         "kernel_avg_note": "HIP-event duration of each trace launch on its stream; with frames "
-                                            "in flight a launch's span includes time shared with the next frame",
                          "bytes_per_launch": int(bytes_launch), "launches_per_step": round(launches_per_step, 3),
-                         "variant": kinfo,
-                         "note": "achieved = logical scene + sample-buffer bytes (DESIGN.md §5); small scenes "
-                                 "are served from LDS, so frac may exceed 1; traffic = PMC HBM bytes per launch"},
-            "valu": {"achieved_tflops": round(flops_launch / (kern_avg_ms * 1e-3) / 1e12, 2),
-                     "peak_tflops": VALU_PEAK_TFLOPS,
-                     "issue_util": pmc.get("valu_issue_util"), "lane_util": pmc.get("valu_lane_util"),
-                     "note": "achieved = counted box/triangle flops; issue_util / lane_util from the committed "
-                             "SQ counter pass (profiles/pmc.json): the kernel is bound by VALU issue under "
-                             "divergence, not by HBM"},
+                         "variant": kinfo, "kernel_sha": sha, "pmc": pmc_state,
+                         "note": "bound: the binding resource is VALU issue under divergence (valu_issue_util = "
+                                 "2 cycles x SQ_INSTS_VALU / (1024 SIMDs x dispatch cycles); valu_lane_util = "
+                                 "active lanes per VALU instruction / 64). achieved/frac: SURVEY.md §8(d) "
+                                 "algorithmic bytes (32 B per node visit, 48 per triangle test, 48 per shadow "
+                                 "query's light point, 12 per pixel) over the HIP-event kernel duration against "
+                                 "the 8 TB/s HBM peak; traffic / hbm_measured_frac: PMC FETCH_SIZE x 2 + "
+                                 "WRITE_SIZE per launch (profiles/pmc.json, only when measured on this "
+                                 "kernel_sha and variant, else null). The scene is LDS-resident for the Cornell "
+                                 "box, so the algorithmic bytes never reach HBM."},
+            "valu": {"achieved_tflops": round(flops_launch / kern_s / 1e12, 2),
+                     "peak_tflops": VALU_PEAK_TFLOPS, "issue_util": issue, "lane_util": lane,
+                     "note": "achieved = counted box/triangle flops (20 per box test, 45 per triangle test)"},
             "lds": ({"achieved": round(scene_gbs, 2), "peak": LDS_PEAK_GBS, "unit": "GB/s",
                      "frac": round(scene_gbs / LDS_PEAK_GBS, 4),
                      "note": "LDS-resident scene: the algorithmic node/triangle bytes are LDS reads, so this, "

@@ -39,6 +39,20 @@ def _stale():
     return any(os.path.getmtime(p) > t for p in deps if os.path.exists(p))
 
 
+def kernel_sha():
+    """Short SHA-256 of the device/host sources and compile flags of libprt: keys the PMC
+    summaries in profiles/pmc.json to the kernel build they were measured on (bench.py marks
+    counter figures of another build as stale instead of reporting them)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(SOURCES + HEADERS + [TRACE_INST]):
+        h.update(f.encode())
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
 def _jobs():
     n = os.environ.get("MAX_JOBS") or os.cpu_count() or 4
     return max(1, min(int(n), 16))

@@ -46,3 +46,13 @@ def test_cpu_leg_reports():
     from pyrenderer_amd.flatten import flatten_scene
     rep, ids, sums = bench.numpy_baseline(flatten_scene(scene), cam.convert_to_taichi_camera().packed(), args, 0.2)
     assert rep["kind"] == "port" and rep["value"] > 0 and sums.shape == (len(ids) * 64, 3)
+
+
+def test_host_cpu_and_kernel_sha(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    t, aff, model = bench.host_cpu()
+    assert t == min(3, aff) and aff >= 1
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.host_cpu()[0] == aff
+    from pyrenderer_amd.build import kernel_sha
+    assert kernel_sha() == kernel_sha() and len(kernel_sha()) == 16

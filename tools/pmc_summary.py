@@ -9,6 +9,10 @@ Collect on the GPU box (one counter pass each; tools/profile_bench.sh does all o
 Then:
     python tools/pmc_summary.py --dir OUT --key cornell_512x512x64spp_d8
 
+The entry records the kernel build (`kernel_sha`, pyrenderer_amd.build.kernel_sha()) and the
+trace-kernel variant the counters were measured on, read from OUT/bench.json (the bench line
+of the same profile run); bench.py reports the counter figures only for that build and variant.
+
 HBM bytes (MI355X_MICROARCH.md §HBM): FETCH_SIZE / WRITE_SIZE are KiB per dispatch summed over
 XCDs; on gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads, so the stored
 `hbm_bytes_per_launch` = 2 x FETCH + WRITE is an upper bound (the raw sum is kept too).
@@ -71,6 +75,12 @@ def main():
                   "valu_lane_util": round(med(sq, "SQ_THREAD_CYCLES_VALU") / (64.0 * med(sq, "SQ_ACTIVE_INST_VALU")), 4)})
     if not e:
         raise SystemExit("no matching dispatches")
+    bl = os.path.join(a.dir, "bench.json")
+    if not os.path.exists(bl):
+        raise SystemExit(f"{bl} missing: the bench line of the profiled run names the kernel build")
+    rl = json.loads(open(bl).read().strip().splitlines()[-1])["roofline"]
+    e["kernel_sha"] = rl["kernel_sha"]
+    e["variant"] = rl["variant"]["variant"]
     e["note"] = ("FETCH_SIZE doubled per the gfx950 correction (upper bound); VALU issue utilisation = "
                  "2 cycles per wave64 instruction on a SIMD-32 over SIMDs x dispatch cycles")
     db = json.load(open(a.out)) if os.path.exists(a.out) else {}
