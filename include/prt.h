@@ -198,7 +198,8 @@ int prt_last_stats(void* scene, uint64_t* stats4);
  * wave-level shader clocks spent in work refill / traversal / shading, wave
  * loop iterations, and active lanes summed over iterations; [11] [12] lane-level
  * inner / leaf traversal trips, [13] deepest traversal stack, [14] samples whose
- * radiance came out NaN or infinite (failure detection; 0 for a sound scene) */
+ * radiance came out NaN or infinite (failure detection; 0 for a sound scene), [15]
+ * wave-level triangle-loop trips (max leaf size over the lanes of each leaf trip) */
 int prt_diag_stats(void* scene, uint64_t* stats16);
 
 #ifdef __cplusplus

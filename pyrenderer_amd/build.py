@@ -58,15 +58,20 @@ def _jobs():
     return max(1, min(int(n), 16))
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, out=None, defs=()):
+    """Build libprt.so (or, for A/B experiments, a copy at `out` compiled with extra -D `defs`)."""
+    lib = out or LIB
+    if out is None and not force and not _stale():
         return LIB
-    os.makedirs(OBJ_DIR, exist_ok=True)
+    obj_dir = OBJ_DIR if out is None else os.path.join("/tmp", "prt_ab_obj", os.path.basename(os.path.splitext(out)[0]))
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(os.path.abspath(lib)), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    units = [(os.path.join(CSRC, f), os.path.join(OBJ_DIR, os.path.splitext(f)[0] + ".o"), []) for f in SOURCES]
-    units += [(os.path.join(CSRC, TRACE_INST), os.path.join(OBJ_DIR, f"prt_trace_{st}_{tt}.o"),
+    extra = [f"-D{d}" for d in defs]
+    units = [(os.path.join(CSRC, f), os.path.join(obj_dir, os.path.splitext(f)[0] + ".o"), []) for f in SOURCES]
+    units += [(os.path.join(CSRC, TRACE_INST), os.path.join(obj_dir, f"prt_trace_{st}_{tt}.o"),
                [f"-DPRT_STACK={st}", f"-DPRT_STATS={tt}"]) for st, tt in TRACE_SETS]
-    cmds = [[hipcc] + FLAGS + defs + ["-c", src, "-o", obj] for src, obj, defs in units]
+    cmds = [[hipcc] + FLAGS + extra + d + ["-c", src, "-o", obj] for src, obj, d in units]
     if verbose:
         print(f"compiling {len(cmds)} units with {_jobs()} jobs", flush=True)
     from concurrent.futures import ThreadPoolExecutor
@@ -80,14 +85,20 @@ def build(force=False, verbose=False):
             raise subprocess.CalledProcessError(r.returncode, cmds[i])
         if verbose and (r.stderr or r.stdout).strip():
             print(r.stdout + r.stderr, flush=True)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + [obj for _, obj, _ in units] + ["-ldl"]
     if verbose:
         print(" ".join(link), flush=True)
     subprocess.check_call(link)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--out", help="A/B copy of the library (e.g. abtmp/libprt_x.so)")
+    ap.add_argument("--define", "-D", action="append", default=[], help="extra preprocessor definition")
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=True, out=a.out, defs=a.define))

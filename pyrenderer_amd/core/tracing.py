@@ -19,6 +19,9 @@ pyrenderer_amd.distributed (torch.distributed gather over RCCL/xGMI).
 per GUI frame, pixels += L, samples += 1, finish() of the running mean), with
 save / load to resume an accumulation.
 """
+import hashlib
+import os
+
 import numpy as np
 
 from ..device_scene import interleaved_tiles, render_multi, unpack_tiles
@@ -96,7 +99,9 @@ class Accumulator:
     leaves the sums bit-identical to `render(spp=N)` * N.  `mean()` is
     pixels / samples (main_taichi.py:61-64, before the sqrt tone map).  `save(path)` /
     `Accumulator.load(path, scene, camera)` resume an accumulation (.npz: sums, sample
-    count, seed, depth, resolution, tile).
+    count, seed, depth, resolution, tile, estimator flags, the packed camera and a
+    fingerprint of the flattened scene — load() refuses a different camera or scene,
+    whose samples would otherwise be averaged into the same image).
     """
 
     def __init__(self, scene, camera, *, depth, seed=0, resolution=None, device=0, tile=64, world=None,
@@ -133,23 +138,45 @@ class Accumulator:
     def state(self):
         return dict(slots=self.slots, samples=np.int64(self.samples), seed=np.int64(self.seed),
                     depth=np.int64(self.depth), resolution=np.array([self.W, self.H], np.int64),
-                    tile=np.int64(self.tile), flags=np.int64(self.flags))
+                    tile=np.int64(self.tile), flags=np.int64(self.flags), camera=self.cam,
+                    scene_sha=np.array(scene_fingerprint(self.world.flat)))
+
+    @staticmethod
+    def state_path(path):
+        """np.savez appends '.npz' to a path without it: save and load use the same name."""
+        path = os.fspath(path)
+        return path if path.endswith(".npz") else path + ".npz"
 
     def save(self, path):
-        np.savez(path, **self.state())
+        np.savez(self.state_path(path), **self.state())
 
     @classmethod
     def load(cls, path, scene, camera, device=0, world=None):
-        z = np.load(path, allow_pickle=False)
+        z = np.load(cls.state_path(path), allow_pickle=False)
         W, H = (int(v) for v in z["resolution"])
         mis = "flags" in z.files and int(z["flags"]) & nee_flags("mis")
         acc = cls(scene, camera, depth=int(z["depth"]), seed=int(z["seed"]), resolution=(W, H), device=device,
                   tile=int(z["tile"]), world=world, nee="mis" if mis else "reference")
         if z["slots"].shape != acc.slots.shape:
             raise ValueError("saved accumulation does not match the frame layout")
+        if "camera" in z.files and not np.array_equal(z["camera"], acc.cam):
+            raise ValueError("saved accumulation was rendered with a different camera")
+        if "scene_sha" in z.files and str(z["scene_sha"]) != scene_fingerprint(acc.world.flat):
+            raise ValueError("saved accumulation was rendered from a different scene")
         acc.slots[...] = z["slots"]
         acc.samples = int(z["samples"])
         return acc
+
+
+def scene_fingerprint(flat):
+    """SHA-256 (hex, 16 chars) of the flattened scene arrays the kernel renders."""
+    h = hashlib.sha256()
+    for k in ("tri_v", "tri_n", "tri_mat", "mat", "light_tri", "light_off", "direct_rgb", "sph", "sph_mat"):
+        a = getattr(flat, k, None)
+        if a is not None:
+            a = np.ascontiguousarray(a)
+            h.update(k.encode() + str(a.dtype).encode() + str(a.shape).encode() + a.tobytes())
+    return h.hexdigest()[:16]
 
 
 def as_image(radiance_xy):

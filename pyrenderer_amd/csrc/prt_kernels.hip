@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float
     if (i >= n) return;
     float4 a = rays[2 * i], b = rays[2 * i + 1];
     V3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
-    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int hid = -1;
     float ht = 0.0f;
     bool hit = traverse_ww4<false, ANY ? 2 : 1, LdsStack, QN>(P.nodes, P.tris, o, d, a.w, b.w, ANY, stk, hid, ht, cn,
@@ -132,6 +132,7 @@ size_t lds_scene_bytes(const TraceParams& P) {
 
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
     size_t b = (size_t)stack * kBlock * sizeof(int);
+    if (variant_spreads(var)) b += (size_t)kSpreadBytesPerWave * (kBlock / 64);
     if (variant_uses_lds(var)) b += lds_scene_bytes(P);
     return b;
 }
@@ -203,6 +204,24 @@ bool variant_quantized(int var) {
 bool variant_spills(int var) {
     switch (var) {
 #define X(id, bits, lds, wpe) case id: return (bits & 32) != 0;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
+bool variant_wide8(int var) {
+    switch (var) {
+#define X(id, bits, lds, wpe) case id: return (bits & 1024) != 0;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
+bool variant_spreads(int var) {
+    switch (var) {
+#define X(id, bits, lds, wpe) case id: return (bits & 512) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;

@@ -60,9 +60,18 @@ def main(argv=None):
     if args.interval > 0 or args.state:
         if len(args.devices) != 1:
             raise SystemExit("progressive rendering (--interval/--state) runs on one device")
-        if args.state and os.path.exists(args.state):
-            acc = Accumulator.load(args.state, scene, camera, device=args.devices[0])
-            print(f"resumed {args.state}: {acc.samples} spp")
+        state = Accumulator.state_path(args.state) if args.state else None
+        if state and os.path.exists(state):
+            acc = Accumulator.load(state, scene, camera, device=args.devices[0])
+            # the saved estimator settings win; refuse a command line that asks for others
+            given = {"depth": args.depth, "seed": args.seed, "resolution": (W, H),
+                     "nee": args.nee}
+            saved = {"depth": acc.depth, "seed": acc.seed, "resolution": (acc.W, acc.H),
+                     "nee": "mis" if acc.flags else "reference"}
+            clash = [f"--{k} {given[k]} (saved: {saved[k]})" for k in given if given[k] != saved[k]]
+            if clash:
+                raise SystemExit(f"{state} was rendered with other settings: " + ", ".join(clash))
+            print(f"resumed {state}: {acc.samples} spp")
         else:
             acc = Accumulator(scene, camera, depth=args.depth, seed=args.seed, resolution=(W, H),
                               device=args.devices[0], nee=args.nee)
@@ -73,9 +82,10 @@ def main(argv=None):
             acc.add(n)
             dt = time.perf_counter() - t
             print(f"{n / dt:.2f} samples/s ({acc.samples} spp, {W * H * n / dt / 1e6:.1f} Msamples/s)", flush=True)
-            if args.state:
-                acc.save(args.state)
+            if state:
+                acc.save(state)
         mean = acc.mean()
+        W, H = acc.W, acc.H
     else:
         mean = render(scene, camera, spp=args.samples, depth=args.depth, seed=args.seed, resolution=(W, H),
                       devices=tuple(args.devices), nee=args.nee)

@@ -100,3 +100,37 @@ def test_cli_progressive_resume_equals_one_render(tmp_path, cornell):
     m2 = main(common + ["--samples", "2", "--nee", "mis", "--out", "", "--tonemap", "reinhard"])
     assert np.isfinite(m2).all() and not np.array_equal(m2, render(cornell[0], cornell[1], spp=2, depth=8, seed=3,
                                                                      resolution=(48, 32)))
+
+
+def test_cli_resume_state_path_and_mismatches(tmp_path, cornell):
+    """a --state path without '.npz' must resume (np.savez appends the suffix),
+    a resumed run must refuse other --depth / --seed / --resolution / --nee, and
+    Accumulator.load must refuse another camera or scene."""
+    import pytest
+    from pyrenderer_amd.core.tracing import Accumulator, render
+    from pyrenderer_amd.main import main
+    state = str(tmp_path / "acc")                      # no suffix
+    common = ["--resolution", "48", "32", "--depth", "6", "--seed", "4"]
+    main(common + ["--samples", "2", "--state", state, "--out", ""])
+    assert (tmp_path / "acc.npz").exists()
+    mean = main(common + ["--samples", "5", "--state", state, "--out", ""])
+    np.testing.assert_array_equal(mean, render(cornell[0], cornell[1], spp=5, depth=6, seed=4, resolution=(48, 32)))
+    for bad in (["--depth", "7"], ["--seed", "5"], ["--nee", "mis"]):
+        args = common + ["--samples", "8", "--state", state, "--out", ""] + bad
+        with pytest.raises(SystemExit, match="other settings"):
+            main(args)
+    with pytest.raises(SystemExit, match="other settings"):
+        main(["--resolution", "32", "32", "--depth", "6", "--seed", "4", "--samples", "8", "--state", state,
+              "--out", ""])
+    scene, camera, _ = cornell
+    import copy
+    moved = copy.deepcopy(camera)
+    moved.iview = moved.iview.copy()
+    moved.iview[0, 3] += 0.25
+    with pytest.raises(ValueError, match="camera"):
+        Accumulator.load(state, scene, moved)
+    from test_multi_light import _scene_json
+    from pyrenderer_amd.io_utils.read_tungsten import read_file
+    other, ocam = read_file(_scene_json(tmp_path))
+    with pytest.raises(ValueError, match="scene"):
+        Accumulator.load(state, other, camera)

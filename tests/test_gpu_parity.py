@@ -191,7 +191,7 @@ def test_all_kernel_variants_bit_identical(gpu_scene, oracle_scene, cornell):
     ids = interleaved_tiles(64, 64, 32)
     o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=2)
     from pyrenderer_amd import _native as N
-    for v in range(1, N.VAR_LAST + 1):
+    for v in N.VAR_REFERENCE:
         g, _ = gpu_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 2, v << 8)
         assert np.array_equal(g, o), v
 
@@ -333,7 +333,7 @@ def test_mis_direct_lighting_variant_matches_oracle(gpu_scene, oracle_scene, cor
     with pytest.raises(N.PrtError):
         gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, N.PRT_FLAG_MIS_NEE | (N.VAR_LDS << 8))
     with pytest.raises(N.PrtError):
-        gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, (N.VAR_MIS[1] + 1) << 8)   # unknown id
+        gpu_scene.render_tiles(cam, W, H, 32, 32, ids, 1, depth, 4, (N.VAR_LAST + 1) << 8)   # unknown id
 
 
 def test_mis_variant_on_a_global_scene_matches_oracle(cornell):

@@ -80,6 +80,7 @@ def main():
                                                  "leaf_simd_eff": round(dg[12] / max(dg[10] * 64, 1), 3),
                                                  "wave_inner_trips_per_iter": round(dg[9] / max(dg[7], 1), 2),
                                                  "wave_leaf_trips_per_iter": round(dg[10] / max(dg[7], 1), 2),
+                                                 "wave_tri_trips_per_iter": round(dg[15] / max(dg[7], 1), 2),
                                                  "max_stack": int(dg[13])}}),
               flush=True)
     for v, rows in res.items():
