@@ -201,6 +201,10 @@ int prt_last_stats(void* scene, uint64_t* stats4);
  * radiance came out NaN or infinite (failure detection; 0 for a sound scene), [15]
  * wave-level triangle-loop trips (max leaf size over the lanes of each leaf trip) */
 int prt_diag_stats(void* scene, uint64_t* stats16);
+/* the same diagnostic words and any beyond them, n of them (unknown words read 0):
+ * [16] most BVH node visits of one query, [23] queries with > 1000 node visits, [24 + 8k ..]
+ * the first 16 of them: o.xyz, d.xyz, t_max (f32 bits), query kind << 32 | node visits */
+int prt_diag_words(void* scene, uint64_t* out, int n);
 
 #ifdef __cplusplus
 }

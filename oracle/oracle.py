@@ -52,7 +52,7 @@ def lib():
                                       _i32, _vp]
         L.or_scene_destroy.argtypes = [_vp]
         L.or_set_trig_mode.argtypes = [_i]
-        L.or_scene_set_bvh.argtypes = [_vp, _vp, _i64, _vp]
+        L.or_scene_set_bvh.argtypes = [_vp, _vp, _i64, _vp, _i64]
         L.or_ref_bvh.argtypes = [_vp] + [_vp] * 6
         L.or_mt.argtypes = [_vp] * 5 + [_f, _f, _vp]
         L.or_aabb.argtypes = [_vp] * 4 + [_f, _f]
@@ -140,7 +140,7 @@ class OracleScene:
         nodes = _f32(nodes, (-1, 16))
         order = np.ascontiguousarray(order, np.int32)
         self._keep += [nodes, order]
-        lib().or_scene_set_bvh(self.h, _p(nodes), nodes.shape[0], _p(order))
+        lib().or_scene_set_bvh(self.h, _p(nodes), nodes.shape[0], _p(order), order.shape[0])
 
     def ref_bvh(self):
         n = 2 * self.n_prim

@@ -649,14 +649,16 @@ static Hit hit_all_bvh(const OScene* s, v3 ro, v3 rd, float t_min, float t_max, 
     return h;
 }
 
-OR_API int or_scene_set_bvh(void* p, const float* nodes, int64_t n_nodes, const int32_t* order) {
+/* order: BVH slot -> triangle, n_order entries (>= n_tri: the build may reference a large
+ * triangle from several leaves, early split clipping; each slot is tested like a leaf entry) */
+OR_API int or_scene_set_bvh(void* p, const float* nodes, int64_t n_nodes, const int32_t* order, int64_t n_order) {
     OScene* s = (OScene*)p;
     free(s->xnode); free(s->xorder);
     s->x_nodes = n_nodes;
     s->xnode = (float*)malloc(sizeof(float) * 16 * n_nodes);
-    s->xorder = (int32_t*)malloc(sizeof(int32_t) * (s->n_tri > 0 ? s->n_tri : 1));
+    s->xorder = (int32_t*)malloc(sizeof(int32_t) * (n_order > 0 ? n_order : 1));
     memcpy(s->xnode, nodes, sizeof(float) * 16 * n_nodes);
-    memcpy(s->xorder, order, sizeof(int32_t) * s->n_tri);
+    memcpy(s->xorder, order, sizeof(int32_t) * n_order);
     return 0;
 }
 

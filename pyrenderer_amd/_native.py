@@ -69,6 +69,7 @@ EXPORTS = {
     "prt_check_faults": (_i, [_vp]),
     "prt_last_stats": (_i, [_vp, _vp]),
     "prt_diag_stats": (_i, [_vp, _vp]),
+    "prt_diag_words": (_i, [_vp, _vp, _i]),
 }
 
 

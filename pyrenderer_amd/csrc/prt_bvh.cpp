@@ -154,6 +154,96 @@ struct Builder {
 
 inline float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
 
+// ---------------------------------------------------------- early split clipping
+// A triangle far larger than the scene's typical one (the Cornell walls among config 4's
+// million small cube faces) would otherwise sit deep in the tree and inflate the box of
+// every ancestor to the wall's size, so every ray near the wall walks those subtrees
+// (config 4: up to 2067 node visits in one query against 25 on average).  Such a
+// triangle enters the build as several references, each the triangle clipped to one cell
+// of a recursive midpoint split of its box (Ernst & Greiner 2007, "early split
+// clipping").  The triangle record is the same for every reference, so traversal tests
+// the same Moller-Trumbore on it, possibly more than once, and the closest (t, id) is
+// unchanged; the reference boxes only have to cover the triangle, which they do: each
+// is the bound of the triangle clipped to its cell (Sutherland-Hodgman in double),
+// rounded outward to f32, and then padded like every other box.
+struct RefBox { double lo[3], hi[3]; };
+
+// bounds of triangle `v` (3 x xyz, double) clipped to box `c`; false when they do not meet
+bool clip_bounds(const double v[3][3], const RefBox& c, RefBox* out) {
+    double poly[16][3], tmp[16][3];
+    int n = 3;
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) poly[i][k] = v[i][k];
+    for (int ax = 0; ax < 3 && n > 0; ++ax)
+        for (int side = 0; side < 2 && n > 0; ++side) {
+            const double b = side == 0 ? c.lo[ax] : c.hi[ax];
+            auto inside = [&](const double* p) { return side == 0 ? p[ax] >= b : p[ax] <= b; };
+            int m = 0;
+            for (int i = 0; i < n; ++i) {
+                const double* a = poly[i];
+                const double* q = poly[(i + 1) % n];
+                const bool ia = inside(a), iq = inside(q);
+                if (ia) { for (int k = 0; k < 3; ++k) tmp[m][k] = a[k]; ++m; }
+                if (ia != iq && m < 15) {
+                    const double t = (b - a[ax]) / (q[ax] - a[ax]);
+                    for (int k = 0; k < 3; ++k) tmp[m][k] = a[k] + t * (q[k] - a[k]);
+                    tmp[m][ax] = b;
+                    ++m;
+                }
+            }
+            n = m;
+            for (int i = 0; i < n; ++i)
+                for (int k = 0; k < 3; ++k) poly[i][k] = tmp[i][k];
+        }
+    if (n == 0) return false;
+    for (int k = 0; k < 3; ++k) { out->lo[k] = INFINITY; out->hi[k] = -INFINITY; }
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < 3; ++k) {
+            out->lo[k] = std::min(out->lo[k], poly[i][k]);
+            out->hi[k] = std::max(out->hi[k], poly[i][k]);
+        }
+    for (int k = 0; k < 3; ++k) {   // the polygon lies in the cell up to rounding
+        out->lo[k] = std::max(out->lo[k], c.lo[k]);
+        out->hi[k] = std::min(out->hi[k], c.hi[k]);
+    }
+    return true;
+}
+
+double ref_area(const RefBox& b) {
+    double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+void split_refs(const double v[3][3], const RefBox& cell, double thr, int depth, std::vector<RefBox>* out) {
+    RefBox b;
+    if (!clip_bounds(v, cell, &b)) return;
+    if (ref_area(b) <= thr || depth >= 12) {
+        out->push_back(b);
+        return;
+    }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k)
+        if (b.hi[k] - b.lo[k] > b.hi[ax] - b.lo[ax]) ax = k;
+    const double mid = 0.5 * (b.lo[ax] + b.hi[ax]);
+    RefBox l = b, r = b;
+    l.hi[ax] = mid;
+    r.lo[ax] = mid;
+    split_refs(v, l, thr, depth + 1, out);
+    split_refs(v, r, thr, depth + 1, out);
+}
+
+inline Box outward_f32(const RefBox& r, const Box& tri_box) {
+    Box b;
+    for (int k = 0; k < 3; ++k) {
+        float lo = (float)r.lo[k], hi = (float)r.hi[k];
+        if ((double)lo > r.lo[k]) lo = std::nextafter(lo, -INFINITY);
+        if ((double)hi < r.hi[k]) hi = std::nextafter(hi, INFINITY);
+        b.lo[k] = std::max(lo, tri_box.lo[k]);   // never beyond the triangle's own box
+        b.hi[k] = std::min(hi, tri_box.hi[k]);
+    }
+    return b;
+}
+
 }  // namespace
 
 bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, std::string* err) {
@@ -164,11 +254,10 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     if (const char* e = std::getenv("PRT_SAH_BINS")) B.bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
     if (const char* e = std::getenv("PRT_SAH_CT")) B.ct = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("PRT_LEAF_MIN")) B.leaf_min = std::max(1, std::min(max_leaf, std::atoi(e)));
-    B.tb.resize((size_t)n_tri);
-    B.cen.resize((size_t)n_tri * 3);
-    B.idx.resize((size_t)n_tri);
+    std::vector<Box> tri_box((size_t)n_tri);
     Box scene;
     float max_abs = 0.0f;
+    double mean_area = 0.0;
     for (int64_t i = 0; i < n_tri; ++i) {
         const float* t = tri_v + 9 * i;
         Box b;
@@ -177,10 +266,50 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
             if (!std::isfinite(t[k])) { *err = "non-finite vertex in triangle " + std::to_string(i); return false; }
             max_abs = std::max(max_abs, std::fabs(t[k]));
         }
-        B.tb[(size_t)i] = b;
+        tri_box[(size_t)i] = b;
+        mean_area += b.area();
+        scene.grow(b);
+    }
+    mean_area /= (double)std::max<int64_t>(n_tri, 1);
+    // references: one per triangle, several (early split clipping) for triangles whose box
+    // area exceeds esc_beta x the mean (env PRT_ESC_BETA, 0 = off; at most 2 n_tri + 4096)
+    double esc_beta = 64.0;
+    if (const char* e = std::getenv("PRT_ESC_BETA")) esc_beta = std::max(0.0, std::atof(e));
+    std::vector<int32_t> ref_tri;
+    ref_tri.reserve((size_t)n_tri);
+    const int64_t ref_cap = 2 * n_tri + 4096;
+    std::vector<RefBox> pieces;
+    for (int64_t i = 0; i < n_tri; ++i) {
+        const Box& b = tri_box[(size_t)i];
+        pieces.clear();
+        if (esc_beta > 0.0 && b.area() > esc_beta * mean_area && (int64_t)B.tb.size() < ref_cap) {
+            const float* t = tri_v + 9 * i;
+            double v[3][3];
+            for (int a = 0; a < 3; ++a)
+                for (int k = 0; k < 3; ++k) v[a][k] = (double)t[3 * a + k];
+            RefBox cell;
+            for (int k = 0; k < 3; ++k) { cell.lo[k] = b.lo[k]; cell.hi[k] = b.hi[k]; }
+            split_refs(v, cell, esc_beta * mean_area, 0, &pieces);
+        }
+        if (pieces.size() <= 1) {
+            B.tb.push_back(b);
+            ref_tri.push_back((int32_t)i);
+        } else {
+            for (const RefBox& r : pieces) {
+                B.tb.push_back(outward_f32(r, b));
+                ref_tri.push_back((int32_t)i);
+            }
+        }
+    }
+    const int64_t n_ref = (int64_t)B.tb.size();
+    if (n_ref >= ((int64_t)1 << 27)) { *err = "too many BVH references (< 2^27)"; return false; }
+    B.n = n_ref;
+    B.cen.resize((size_t)n_ref * 3);
+    B.idx.resize((size_t)n_ref);
+    for (int64_t i = 0; i < n_ref; ++i) {
+        const Box& b = B.tb[(size_t)i];
         for (int k = 0; k < 3; ++k) B.cen[3 * (size_t)i + k] = 0.5f * (b.lo[k] + b.hi[k]);
         B.idx[(size_t)i] = (int32_t)i;
-        scene.grow(b);
     }
     float extent = scene.valid() ? std::max({scene.hi[0] - scene.lo[0], scene.hi[1] - scene.lo[1], scene.hi[2] - scene.lo[2]}) : 0.0f;
     // Padding: ~8 ulps of the largest coordinate magnitude / extent.  Keeps the
@@ -188,9 +317,9 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     // lie a rounding error outside the triangle (axis-aligned Cornell edges).
     float pad = std::max(max_abs, extent) * 1e-6f + 1e-30f;
     int32_t root = -1;
-    if (n_tri > 0) {
-        B.nodes.reserve((size_t)(2 * n_tri / std::max(1, max_leaf / 2) + 8));
-        root = B.build(0, n_tri, 0);
+    if (n_ref > 0) {
+        B.nodes.reserve((size_t)(2 * n_ref / std::max(1, max_leaf / 2) + 8));
+        root = B.build(0, n_ref, 0);
     }
     // flatten: inner nodes in DFS preorder; leaves become child references
     std::vector<int32_t> inner_id(B.nodes.size(), -1);
@@ -232,7 +361,7 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
         Box empty;
         if (root >= 0) put_box(f, 0, B.nodes[root].box, true); else put_box(f, 0, empty, false);
         put_box(f, 1, empty, false);
-        int32_t lr = root >= 0 ? leaf_ref(0, (int)n_tri) : leaf_ref(0, 1);
+        int32_t lr = root >= 0 ? leaf_ref(0, (int)n_ref) : leaf_ref(0, 1);
         f[12] = bits_f(lr); f[13] = bits_f(lr); f[14] = 0.0f; f[15] = 0.0f;
         out->n_nodes = 1;
     } else {
@@ -247,10 +376,11 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
         }
         out->n_nodes = n_inner;
     }
-    out->order = B.idx;
-    out->tris.assign((size_t)n_tri * 12, 0.0f);
-    for (int64_t s = 0; s < n_tri; ++s) {
-        int32_t o = B.idx[(size_t)s];
+    out->order.resize((size_t)n_ref);
+    for (int64_t s = 0; s < n_ref; ++s) out->order[(size_t)s] = ref_tri[(size_t)B.idx[(size_t)s]];
+    out->tris.assign((size_t)n_ref * 12, 0.0f);
+    for (int64_t s = 0; s < n_ref; ++s) {
+        int32_t o = out->order[(size_t)s];
         const float* t = tri_v + 9 * (int64_t)o;
         float* d = out->tris.data() + 12 * s;
         for (int k = 0; k < 3; ++k) {
@@ -260,7 +390,8 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
         }
         d[3] = bits_f(o); d[7] = 0.0f; d[11] = 0.0f;
     }
-    out->depth = n_tri > 0 ? std::max(1, B.max_depth) : 1;
+    out->depth = n_ref > 0 ? std::max(1, B.max_depth) : 1;
+    out->n_refs = n_ref;
     out->n_leaves = B.leaves;
     out->pad = pad;
     double sah = 0.0;

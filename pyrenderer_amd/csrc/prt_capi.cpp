@@ -69,7 +69,7 @@ void frame_rows(F3 n, float* out12) {
 
 // stats words: nodes, tris, ext, shadow (public) + diagnostic wave clocks
 // (refill, traversal, shading), wave iterations, active lanes at traversal
-constexpr int kStatWords = 16;
+constexpr int kStatWords = 24 + 16 * 8;   // prt_diag_stats' 16 + prt_diag_words' extras (outlier log)
 
 struct DevBuf {
     void* p = nullptr;
@@ -126,6 +126,7 @@ struct Scene {
     uint32_t guard_trips = 1u << 20; // traversal phases per query before the watchdog trips (env PRT_GUARD_TRIPS)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
     int max_leaf = 4;                // BVH leaf size bound (env PRT_MAX_LEAF); spread variants need <= 4
+    std::string wave_clock_path;     // env PRT_WAVE_CLOCK: append each trace launch's per-wave clocks here
     int64_t n_sph = 0;
     DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
     hipStream_t stream = nullptr;
@@ -405,8 +406,26 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         HIP_TRY(hipMemsetAsync(cx->work.p, 0, 16, stream));
         if (primary) HIP_TRY(prt::launch_camera(P, (float4*)cx->rays.p, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
+        DevBuf wclk;
+        if (!s->wave_clock_path.empty()) {
+            HIP_TRY(wclk.ensure(sizeof(unsigned long long) * 3 * (size_t)grid * (256 / 64)));
+            HIP_TRY(hipMemsetAsync(wclk.p, 0, sizeof(unsigned long long) * 3 * (size_t)grid * 4, stream));
+            P.wave_clock = (unsigned long long*)wclk.p;
+        }
         HIP_TRY(prt::launch_trace(P, stack, var, grid, stats, stream));
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k + 1], stream));
+        if (P.wave_clock) {
+            // diagnostic only: synchronous read-back, appended as (start, end, items) u64 triples
+            std::vector<unsigned long long> h((size_t)grid * 4 * 3);
+            HIP_TRY(hipMemcpyAsync(h.data(), wclk.p, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
+                                   stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+            if (FILE* f = std::fopen(s->wave_clock_path.c_str(), "ab")) {
+                std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+                std::fclose(f);
+            }
+            P.wave_clock = nullptr;
+        }
         HIP_TRY(prt::launch_reduce((const float*)cx->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0 && !accumulate,
                                    stream));
     }
@@ -642,12 +661,15 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             rc = fail(PRT_ERR_OOM, std::string("hipMalloc: ") + hipGetErrorString(e));
             break;
         }
+        // the hit-query watchdog flag is read by prt_check_faults before any hit query ran
+        if ((e = hipMemset(s->work.p, 0, 64)) != hipSuccess) { rc = fail(PRT_ERR_HIP, hipGetErrorString(e)); break; }
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) { rc = fail(PRT_ERR_HIP, hipGetErrorString(e)); break; }
         s->cus = prop.multiProcessorCount;
         s->n_tri_f4 = (int64_t)bvh.tris.size() / 4;
         if (const char* le = std::getenv("PRT_LEAF_EXIT")) s->leaf_exit = std::max(0, std::min(64, std::atoi(le)));
         if (const char* lb = std::getenv("PRT_LEAF_BREAK")) s->leaf_break = std::max(0, std::min(64, std::atoi(lb)));
+        if (const char* wc = std::getenv("PRT_WAVE_CLOCK")) s->wave_clock_path = wc;
         if (const char* gt = std::getenv("PRT_GUARD_TRIPS"))
             s->guard_trips = (uint32_t)std::max(1LL, std::min((long long)UINT32_MAX, std::atoll(gt)));
         if (const char* rm = std::getenv("PRT_RESUME_MIN")) s->resume_min = std::max(1, std::min(64, std::atoi(rm)));
@@ -836,6 +858,17 @@ int prt_last_stats(void* scene, uint64_t* stats4) {
     return PRT_OK;
 }
 
+int prt_diag_words(void* scene, uint64_t* out, int n) {
+    auto* s = (Scene*)scene;
+    if (!s || !out || n < 0) return fail(PRT_ERR_ARG, "NULL argument or n < 0");
+    DeviceGuard g(s->device);
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long h[kStatWords];
+    HIP_TRY(hipMemcpy(h, s->stats.p, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n; ++i) out[i] = i < kStatWords ? h[i] : 0;
+    return PRT_OK;
+}
+
 int prt_diag_stats(void* scene, uint64_t* stats16) {
     auto* s = (Scene*)scene;
     if (!s || !stats16) return fail(PRT_ERR_ARG, "NULL argument");
@@ -843,7 +876,7 @@ int prt_diag_stats(void* scene, uint64_t* stats16) {
     HIP_TRY(hipDeviceSynchronize());
     unsigned long long h[kStatWords];
     HIP_TRY(hipMemcpy(h, s->stats.p, sizeof(h), hipMemcpyDeviceToHost));
-    for (int i = 0; i < kStatWords; ++i) stats16[i] = h[i];
+    for (int i = 0; i < 16; ++i) stats16[i] = h[i];
     return PRT_OK;
 }
 

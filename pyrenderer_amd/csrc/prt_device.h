@@ -248,7 +248,7 @@ __device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, f
 }
 
 // ---------------------------------------------------------------- traversal
-struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp, nonfinite, w_tri; };
+struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp, nonfinite, w_tri, q0, max_q; };
 
 // Moller-Trumbore in the reference's exact expression order
 // (intersection_taichi.py:69-91), for closest-hit and any-hit lanes of one wave.
@@ -360,10 +360,18 @@ __device__ __forceinline__ bool qchild(int k, uint32_t lxq, uint32_t hxq, uint32
 
 // Traversal state of a query that may be suspended between loop iterations (RES).
 struct TState { int cur, leaf, sp, best_id; float best; };
+// A query whose t_max is NaN (the reference's shadow bound t_at_light = (p2.x - p.x) / w.x
+// is 0/0 when p2.x == p.x, core/tracing.py:97) can never accept a triangle: Moller-Trumbore
+// needs t < t_max (intersection_taichi.py:84), false against NaN.  Its slab tests never cull
+// either (fminf drops the NaN), so traversing would walk every box along the whole line
+// (config 4: ~2000 node visits, the launch's last 2 ms); it starts finished instead, with
+// the same (miss) result.  Spheres still see the NaN bound (hit_sphere accepts it).
+__device__ __forceinline__ int root_for(float tmax) { return tmax == tmax ? 0 : kSentinel; }
+
 template <class S>
 __device__ __forceinline__ void tstate_init(TState& ts, S stk, float tmax) {
     stk.put(0, kSentinel);
-    ts.cur = 0; ts.leaf = 0; ts.sp = 0; ts.best_id = -1; ts.best = tmax;
+    ts.cur = root_for(tmax); ts.leaf = 0; ts.sp = 0; ts.best_id = -1; ts.best = tmax;
 }
 
 // RES: the wave leaves the traversal loop once fewer than `min_lanes` lanes are still
@@ -390,6 +398,18 @@ __device__ __forceinline__ bool slab_nf(float nx, float fx, float ny, float fy, 
     float tfar = fminf(fminf(bx, by), fminf(bz, tmax)) * kGamma;
     tn = tnear;
     return tnear <= tfar;
+}
+
+// Slab reciprocals 1/d, clamped to +-1e30.  A direction component of exactly +-0 (one cosine
+// draw in 2^24) would give 1/d = +-inf, and fma(plane, 1/d, -o/d) = inf - inf = NaN: the
+// near/far selection then drops that axis and the ray culls nothing along it, walking every
+// box it overlaps in the other two axes (config 4: 1000-2200 node visits for such a query,
+// against 25 on average, each one of the launch's slowest paths).  With the clamp the
+// distances are +-1e30 (plane - o) up to the rounding of o * 1e30 (|o| 2^-24 1e30), which the
+// box padding (>= 1e-6 |o|) covers: the sign is right and the test stays conservative.
+__device__ __forceinline__ V3 ray_inv(V3 d) {
+    auto c = [](float x) { return __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(x), -1e30f, 1e30f); };
+    return v3(c(d.x), c(d.y), c(d.z));
 }
 
 // One inner-node visit of the while-while BVH4 traversal: tests the four child boxes of
@@ -528,7 +548,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                                              int* fault = nullptr, int leaf_break = 0, int leaf_exit = 0,
                                              uint32_t guard_lim = kGuardTrips) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    const V3 inv = ray_inv(d);
     V3 oi = o * inv;
     // near plane index per axis (0 = lo, 1 = hi) from the sign of 1/d
     const int sx = __float_as_int(inv.x) < 0 ? 1 : 0, sy = __float_as_int(inv.y) < 0 ? 1 : 0,
@@ -701,7 +721,7 @@ __device__ __forceinline__ bool traverse_sp(const float4* __restrict__ nodes, co
                                             int leaf_exit, uint32_t guard_lim) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     const int lane = (int)__lane_id();
-    V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+    const V3 inv = ray_inv(d);
     V3 oi = o * inv;
     const int sx = __float_as_int(inv.x) < 0 ? 1 : 0, sy = __float_as_int(inv.y) < 0 ? 1 : 0,
               sz = __float_as_int(inv.z) < 0 ? 1 : 0;
@@ -709,7 +729,7 @@ __device__ __forceinline__ bool traverse_sp(const float4* __restrict__ nodes, co
     float best = tmax;
     int best_id = -1;
     int sp = 0;
-    int cur = part ? 0 : kSentinel;
+    int cur = part ? root_for(tmax) : kSentinel;
     int leaf = 0;
     uint32_t guard = 0;
     while (__ballot(cur != kSentinel || leaf < 0)) {
@@ -885,6 +905,9 @@ void trace_kernel(TraceParams P) {
         s_loff = slo;
     }
     const int lane = threadIdx.x & 63;
+    // diagnostic (P.wave_clock, env PRT_WAVE_CLOCK): each wave's start / end real time
+    const uint64_t t_start = P.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint32_t n_taken = 0;   // items this wave took from the queue (diagnostic)
 
     // wave-uniform work queue [q_next, q_end)
     uint32_t q_next = 0, q_end = 0;
@@ -903,7 +926,7 @@ void trace_kernel(TraceParams P) {
     V3 mis_n = v3(0, 0, 0), mis_n2 = v3(0, 0, 0), mis_fl = v3(0, 0, 0), mis_bd = v3(0, 0, 0);
     float mis_bp = 0.0f;
     float tmax = kTMax;
-    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
     uint32_t chunk_s = 0;   // wave-uniform: sample index (within the launch) of the current chunk
     uint32_t chunk_xy0 = 0; // wave-uniform: origin of the current chunk's tile
@@ -939,6 +962,7 @@ void trace_kernel(TraceParams P) {
                 } else {
                     q_next = base;
                     q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
+                    n_taken += q_end - q_next;
                     // n_slots is a multiple of 64 (tile sizes are powers of two >= 64 px),
                     // so a chunk never straddles two samples: one scalar division per chunk
                     chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
@@ -1022,6 +1046,7 @@ void trace_kernel(TraceParams P) {
         // the drain, with few lanes left, they would switch phase after every trip
         const int lb = exhausted ? 0 : P.leaf_break, le = exhausted ? 0 : P.leaf_exit;
         const uint32_t glim = P.guard_trips;
+        if (STATS && !pending) cn.q0 = cn.nodes;   // node visits at the start of this query
         if (SPREAD) {
             char* sb = reinterpret_cast<char*>(smem) + kStackWords * kBlock * 4;
             const int w = threadIdx.x >> 6;
@@ -1069,6 +1094,20 @@ void trace_kernel(TraceParams P) {
                                                               stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim);
         }
 
+        if (STATS) {
+            const uint32_t qn = cn.nodes - cn.q0;
+            cn.max_q = max(cn.max_q, qn);   // most node visits of one query
+            // outlier log (diag words 24..151): the first 16 queries with > 1000 node visits
+            if (qn > 1000) {
+                const unsigned long long k = atomicAdd(P.stats + 23, 1ull);
+                if (k < 16) {
+                    unsigned long long* r = P.stats + 24 + 8 * k;
+                    r[0] = __float_as_uint(o.x); r[1] = __float_as_uint(o.y); r[2] = __float_as_uint(o.z);
+                    r[3] = __float_as_uint(d.x); r[4] = __float_as_uint(d.y); r[5] = __float_as_uint(d.z);
+                    r[6] = __float_as_uint(tmax); r[7] = ((unsigned long long)qtype << 32) | qn;
+                }
+            }
+        }
         if (P.n_sph > 0 && !(qtype == Q_SHADOW && hit)) {
             // analytic spheres after the triangles (ids n_tri + k), same rule as the oracle
             float best = hit ? ht : tmax;
@@ -1323,6 +1362,12 @@ void trace_kernel(TraceParams P) {
             if (leader) c_shade += __builtin_amdgcn_s_memtime() - t_a;
         }
     }
+    if (P.wave_clock && lane == 0) {
+        const size_t w = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+        P.wave_clock[3 * w] = t_start;
+        P.wave_clock[3 * w + 1] = __builtin_amdgcn_s_memrealtime();
+        P.wave_clock[3 * w + 2] = n_taken;
+    }
     if (STATS) {
         uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
         for (int off = 32; off > 0; off >>= 1) {
@@ -1346,6 +1391,9 @@ void trace_kernel(TraceParams P) {
             uint32_t nf = cn.nonfinite;
             for (int off = 32; off > 0; off >>= 1) nf += (uint32_t)__shfl_down((int)nf, off);
             if (lane == 0 && nf) atomicAdd(P.stats + 14, (unsigned long long)nf);
+            uint32_t mq = cn.max_q;
+            for (int off = 32; off > 0; off >>= 1) mq = max(mq, (uint32_t)__shfl_down((int)mq, off));
+            if (lane == 0) atomicMax(P.stats + 16, (unsigned long long)mq);
             uint32_t wt = cn.w_tri;
             for (int off = 32; off > 0; off >>= 1) wt += (uint32_t)__shfl_down((int)wt, off);
             if (lane == 0 && wt) atomicAdd(P.stats + 15, (unsigned long long)wt);

@@ -27,7 +27,9 @@ inline int32_t leaf_ref(int64_t first, int count) {
 struct BvhHost {
     std::vector<float> nodes;      // n_nodes * 16
     std::vector<float> tris;       // n_tri * 12, BVH order
-    std::vector<int32_t> order;    // BVH slot -> original triangle index
+    std::vector<int32_t> order;    // BVH slot -> original triangle index (a triangle split by early
+                                   // split clipping occupies several slots)
+    int64_t n_refs = 0;            // triangle records in BVH order (>= n_tri)
     int32_t depth = 0;             // max root-to-leaf edge count
     int64_t n_nodes = 0;
     int64_t n_leaves = 0;

@@ -47,6 +47,7 @@ struct TraceParams {
     int n_sph;
     const float4* sph;        // center xyz, radius
     const int* sph_mat;
+    unsigned long long* wave_clock;  // diagnostic: per wave (start, end, items) real-time stamps, or null
 };
 
 // trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the

@@ -62,7 +62,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float
     if (i >= n) return;
     float4 a = rays[2 * i], b = rays[2 * i + 1];
     V3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
-    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int hid = -1;
     float ht = 0.0f;
     bool hit = traverse_ww4<false, ANY ? 2 : 1, LdsStack, QN>(P.nodes, P.tris, o, d, a.w, b.w, ANY, stk, hid, ht, cn,

@@ -174,6 +174,13 @@ class DeviceScene:
         N.check(N.lib().prt_last_stats(self.h, N.ptr(s)))
         return s
 
+    def diag_words(self, n=17):
+        """prt_diag_words: the diagnostic words of the last PRT_FLAG_STATS call, [16] = most node
+        visits of one query."""
+        s = np.zeros(n, np.uint64)
+        N.check(N.lib().prt_diag_words(self.h, N.ptr(s), n))
+        return s
+
     def diag_stats(self):
         """16 diagnostic words of the last PRT_FLAG_STATS call (see include/prt.h)."""
         s = np.zeros(16, np.uint64)

@@ -20,6 +20,8 @@ def load(path):
     from pyrenderer_amd import _native as N
     L = ctypes.CDLL(os.path.abspath(path))
     for name, (res, args) in N.EXPORTS.items():
+        if not hasattr(L, name):   # an older build: entry points added since are not used here
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -77,6 +79,10 @@ def main():
                           "kernel_ms_min": round(float(ms.min()), 4), "kernel_ms_all": [round(float(x), 4) for x in ms],
                           "msamples_s": round(samples / np.median(ms) / 1e3, 1),
                           "identical": all(x[1] for x in rows)}), flush=True)
+    # each scene handle belongs to its own library: destroy it through that library
+    for L, ds in zip(libs, scenes):
+        N._lib = L
+        ds.close()
 
 
 if __name__ == "__main__":

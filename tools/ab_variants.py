@@ -69,7 +69,7 @@ def main():
     from pyrenderer_amd._native import PRT_FLAG_STATS
     for v in a.variants:
         ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, PRT_FLAG_STATS | vflags(v))
-        dg = ds.diag_stats().astype(np.float64)
+        dg = ds.diag_words().astype(np.float64)
         tot = dg[4] + dg[5] + dg[6]
         print(json.dumps({"variant": v, "diag": {"refill_frac": round(dg[4] / tot, 3), "trav_frac": round(dg[5] / tot, 3),
                                                  "shade_frac": round(dg[6] / tot, 3), "wave_iters": int(dg[7]),
@@ -81,7 +81,8 @@ def main():
                                                  "wave_inner_trips_per_iter": round(dg[9] / max(dg[7], 1), 2),
                                                  "wave_leaf_trips_per_iter": round(dg[10] / max(dg[7], 1), 2),
                                                  "wave_tri_trips_per_iter": round(dg[15] / max(dg[7], 1), 2),
-                                                 "max_stack": int(dg[13])}}),
+                                                 "max_stack": int(dg[13]),
+                                                 "max_nodes_one_query": int(dg[16])}}),
               flush=True)
     for v, rows in res.items():
         ms = np.array([x[0] for x in rows])
