@@ -122,7 +122,7 @@ struct Scene {
     int need4 = 0;                   // worst-case BVH4 traversal stack entries
     int leaf_break = -1;             // env PRT_LEAF_BREAK (0..64); -1: per variant (trace launch)
     int leaf_exit = 8;               // env PRT_LEAF_EXIT (0..64); C2 5.25 -> 5.04 ms, C4 29.8 -> 28.8 ms
-    int resume_min = 48;             // resume variants (env PRT_RESUME_MIN; C4 sweep: 16 -> 37.4 ms, 48 -> 34.8 ms)
+    int resume_min = 32;             // resume variants (env PRT_RESUME_MIN; C4 after the r02 BVH fixes: 16 / 24 / 32 / 40 / 48 -> 19.4 / 19.1 / 19.0 / 19.4 / 19.8 ms)
     uint32_t guard_trips = 1u << 20; // traversal phases per query before the watchdog trips (env PRT_GUARD_TRIPS)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
     int max_leaf = 4;                // BVH leaf size bound (env PRT_MAX_LEAF); spread variants need <= 4
