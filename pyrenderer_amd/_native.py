@@ -21,12 +21,9 @@ PRT_FLAG_MIS_NEE = 0x8
 VAR_LDS = 1           # LDS-resident scene, phase-aligned schedule, >= 6 waves/SIMD
 VAR_LDS_ANY_OCC = 2   # ... without the occupancy target
 VAR_GLOBAL = 3        # scene in HBM: quantised BVH4, LDS stack + global spill, suspended tails
-VAR_LDS_SPREAD = 6    # VAR_LDS with the spread leaf phase (every (lane, triangle) pair over all 64 lanes)
-VAR_GLOBAL_SPREAD = 7 # global scene (mixed schedule) with the spread leaf phase
-VAR_GLOBAL8 = 8       # VAR_GLOBAL over the quantised BVH8 (one 128-B node per 8 child boxes)
 VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS_SPREAD, VAR_GLOBAL_SPREAD, VAR_GLOBAL8)
-VAR_LAST = 8
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL)
+VAR_LAST = 5
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 

@@ -545,87 +545,4 @@ void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out) {
     }
 }
 
-// Quantised BVH8 (prt_internal.h): the BVH2 collapsed 8-wide (open the inner child with
-// the largest surface area until a node holds eight children), each node quantised like
-// quantize_bvh4 (u8 grid coordinates per child, rounded outward with >= 2 pad to spare).
-void build_bvh8q(const BvhHost& b2, float pad, Bvh8Host* out) {
-    struct Item { int32_t b2node; int32_t slot; int32_t depth; };
-    std::vector<Item> work;
-    out->nodes.assign(kNode8F4 * 4, 0.0f);
-    out->n_nodes = 1;
-    out->depth = 0;
-    work.push_back({0, 0, 0});
-    const double margin = 2.0 * (double)pad;
-    while (!work.empty()) {
-        Item it = work.back();
-        work.pop_back();
-        const float* n2 = b2.nodes.data() + (size_t)it.b2node * 16;
-        std::vector<Child> ch;
-        for (int side = 0; side < 2; ++side) {
-            Child c = child_of(n2, side);
-            if (!c.empty) ch.push_back(c);
-        }
-        while (ch.size() < 8) {
-            int best = -1;
-            double ba = -1.0;
-            for (size_t k = 0; k < ch.size(); ++k)
-                if (ch[k].ref >= 0 && child_area(ch[k]) > ba) { ba = child_area(ch[k]); best = (int)k; }
-            if (best < 0) break;
-            const float* m = b2.nodes.data() + (size_t)ch[best].ref * 16;
-            Child a = child_of(m, 0), b = child_of(m, 1);
-            ch.erase(ch.begin() + best);
-            if (!a.empty) ch.push_back(a);
-            if (!b.empty) ch.push_back(b);
-        }
-        int32_t refs[8];
-        for (int k = 0; k < 8; ++k) {
-            refs[k] = 0x7FFFFFFF;   // empty slot: the traversal sentinel (and masked by the kernel)
-            if (k < (int)ch.size()) {
-                if (ch[k].ref >= 0) {
-                    refs[k] = (int32_t)out->n_nodes++;
-                    work.push_back({ch[k].ref, refs[k], it.depth + 1});
-                } else {
-                    refs[k] = ch[k].ref;
-                }
-            }
-        }
-        out->nodes.resize((size_t)out->n_nodes * kNode8F4 * 4, 0.0f);
-        float* q = out->nodes.data() + (size_t)it.slot * kNode8F4 * 4;
-        uint32_t ql[3][2] = {{0, 0}, {0, 0}, {0, 0}}, qh[3][2] = {{0, 0}, {0, 0}, {0, 0}};
-        for (int a = 0; a < 3; ++a) {
-            double lo = INFINITY, hi = -INFINITY;
-            for (const Child& c : ch) {
-                lo = std::min(lo, (double)c.lo[a]);
-                hi = std::max(hi, (double)c.hi[a]);
-            }
-            if (!(lo <= hi)) { lo = 0.0; hi = 0.0; }
-            float o = (float)(lo - margin);
-            if ((double)o > lo - margin) o = std::nextafter(o, -INFINITY);
-            double ext = hi + margin - (double)o;
-            float stf = (float)std::max(ext / 254.0, 1e-30);
-            if ((double)stf < ext / 254.0) stf = std::nextafter(stf, INFINITY);
-            const double st = (double)stf;
-            q[a] = o;
-            q[a == 0 ? 3 : 3 + a] = stf;   // s.x at f[0].w, s.y / s.z at f[1].x / f[1].y
-            for (int k = 0; k < (int)ch.size(); ++k) {
-                long l = (long)std::floor(((double)ch[k].lo[a] - margin - (double)o) / st);
-                long h = (long)std::ceil(((double)ch[k].hi[a] + margin - (double)o) / st);
-                l = std::max(0L, std::min(255L, l));
-                h = std::max(0L, std::min(255L, h));
-                ql[a][k >> 2] |= (uint32_t)l << (8 * (k & 3));
-                qh[a][k >> 2] |= (uint32_t)h << (8 * (k & 3));
-            }
-        }
-        // f[1].zw = qlo.x, f[2] = qhi.x qlo.y, f[3] = qhi.y qlo.z, f[4].xy = qhi.z
-        uint32_t words[10] = {ql[0][0], ql[0][1], qh[0][0], qh[0][1], ql[1][0], ql[1][1],
-                              qh[1][0], qh[1][1], ql[2][0], ql[2][1]};
-        std::memcpy(q + 6, words, sizeof(words));
-        std::memcpy(q + 16, &qh[2][0], 4);
-        std::memcpy(q + 17, &qh[2][1], 4);
-        std::memcpy(q + 20, refs, sizeof(refs));
-        out->depth = std::max(out->depth, it.depth);
-    }
-    out->stack_need = 7 * (out->depth + 1) + 2;   // + the sentinel and the slot above the top
-}
-
 }  // namespace prt

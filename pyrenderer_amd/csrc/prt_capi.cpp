@@ -112,9 +112,6 @@ struct Scene {
     float direct_rgb[3] = {0.9f, 0.85f, 0.7f};
     DevBuf nodes4q;                  // quantised BVH4 (prt_internal.h)
     int64_t n_node4q_f4 = 0;
-    DevBuf nodes8q;                  // quantised BVH8 (prt_internal.h)
-    int64_t n_node8q_f4 = 0;
-    int need8 = 0;                   // worst-case BVH8 traversal stack entries
     DevBuf nodes4, tris, tri_nm, tri_frame, mats, light_v, light_off, sph, sph_mat;
     int64_t n_node4_f4 = 0;
     int32_t depth4 = 0;
@@ -125,7 +122,6 @@ struct Scene {
     int resume_min = 32;             // resume variants (env PRT_RESUME_MIN; C4 after the r02 BVH fixes: 16 / 24 / 32 / 40 / 48 -> 19.4 / 19.1 / 19.0 / 19.4 / 19.8 ms)
     uint32_t guard_trips = 1u << 20; // traversal phases per query before the watchdog trips (env PRT_GUARD_TRIPS)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
-    int max_leaf = 4;                // BVH leaf size bound (env PRT_MAX_LEAF); spread variants need <= 4
     std::string wave_clock_path;     // env PRT_WAVE_CLOCK: append each trace launch's per-wave clocks here
     int64_t n_sph = 0;
     DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
@@ -158,7 +154,7 @@ int upload(DevBuf& b, const void* host, size_t bytes, size_t* total) {
 void destroy_scene(Scene* s) {
     if (!s) return;
     DeviceGuard g(s->device);
-    for (DevBuf* b : {&s->nodes4q, &s->nodes8q, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v,
+    for (DevBuf* b : {&s->nodes4q, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v,
                       &s->light_off, &s->sph, &s->sph_mat, &s->work, &s->stats, &s->frame, &s->gather,
                       &s->gather_xy})
         b->release();
@@ -365,12 +361,10 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     if (s->stack4 == 0 && !spill) return fail(PRT_ERR_ARG, "BVH4 too deep for the LDS traversal stack variants");
     const int stack = variant_stack(s, var);
     if (prt::variant_quantized(var)) {
-        P.nodes = (const float4*)(prt::variant_wide8(var) ? s->nodes8q.p : s->nodes4q.p);
-        P.n_node_f4 = (int)(prt::variant_wide8(var) ? s->n_node8q_f4 : s->n_node4q_f4);
+        P.nodes = (const float4*)s->nodes4q.p;
+        P.n_node_f4 = (int)s->n_node4q_f4;
     }
     if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
-    if (prt::variant_spreads(var) && s->max_leaf > 4)
-        return fail(PRT_ERR_ARG, "spread leaf-phase variants need BVH leaves of <= 4 triangles (PRT_MAX_LEAF)");
     // while-while leaf-phase entry: LDS scenes wait for every descending lane's leaf (their
     // leaves are cheap and traversals short); global scenes enter the leaf phase once at
     // most 8 descending lanes still lack one (C4: 35.1 -> 29.7 ms; C2 prefers 0)
@@ -380,8 +374,7 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(stack, var, stats, prt::trace_smem_bytes(stack, var, P)));
     if (spill) {
         // entries [spill_lds, need4] of every lane of the largest grid, plus one slot of headroom
-        const int need = prt::variant_wide8(var) ? s->need8 : s->need4;
-        size_t per_lane = (size_t)std::max(1, need + 2 - s->spill_lds);
+        size_t per_lane = (size_t)std::max(1, s->need4 + 2 - s->spill_lds);
         HIP_TRY(cx->spill.ensure(per_lane * (size_t)occ * s->cus * 256 * sizeof(int)));
         P.spill = (int*)cx->spill.p;
     }
@@ -582,12 +575,10 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
 
     prt::BvhHost bvh;
     std::string err;
-    int leaf_bound = 4;
     try {
         int max_leaf = 4;
         if (const char* ml = std::getenv("PRT_MAX_LEAF")) max_leaf = std::atoi(ml);
         if (!prt::build_bvh(tri_v, n_tri, max_leaf, &bvh, &err)) return fail(PRT_ERR_ARG, err);
-        leaf_bound = max_leaf;
     } catch (const std::bad_alloc&) {
         return fail(PRT_ERR_OOM, "host allocation failed during BVH build");
     }
@@ -597,7 +588,6 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
     s->n_tri = n_tri;
     s->n_nodes = bvh.n_nodes;
     s->depth = bvh.depth;
-    s->max_leaf = leaf_bound;
     s->n_light = n_light;
     s->n_mat = n_mat;
     if (direct_rgb) std::memcpy(s->direct_rgb, direct_rgb, sizeof(float) * 3);
@@ -642,11 +632,6 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             prt::quantize_bvh4(b4, bvh.pad, &q4);
             s->n_node4q_f4 = (int64_t)q4.size() / 4;
             if ((rc = upload(s->nodes4q, q4.data(), sizeof(float) * q4.size(), &s->device_bytes))) break;
-            prt::Bvh8Host b8;
-            prt::build_bvh8q(bvh, bvh.pad, &b8);
-            s->need8 = b8.stack_need;
-            s->n_node8q_f4 = (int64_t)b8.nodes.size() / 4;
-            if ((rc = upload(s->nodes8q, b8.nodes.data(), sizeof(float) * b8.nodes.size(), &s->device_bytes))) break;
         }
         if ((rc = upload(s->tris, bvh.tris.data(), sizeof(float) * bvh.tris.size(), &s->device_bytes))) break;
         if ((rc = upload(s->tri_nm, nm.data(), sizeof(float) * nm.size(), &s->device_bytes))) break;

@@ -483,65 +483,7 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     else step(stk);
 }
 
-// One visit of a quantised BVH8 node (prt_internal.h Bvh8Host): eight child boxes from one
-// 128-B line.  Closest-hit (MODE 0 / 1): the nearest hit child is visited next and the other
-// hit children pushed in slot order (no sorting network); any-hit (MODE 2): the last hit
-// child next, the others pushed.  Empty slots carry the sentinel ref and are masked.
-template <bool STATS, int MODE, class S>
-__device__ __forceinline__ void visit_node8q(const float4* __restrict__ nodes, int& cur, int& sp, S stk, V3 inv,
-                                             V3 oi, int sx, int sy, int sz, float tmin, float best, Counters& cn) {
-    const float4* nd = nodes + (size_t)cur * 8;
-    const float4 a = nd[0], b = nd[1], c = nd[2], e = nd[3], g = nd[4], ra = nd[5], rb = nd[6];
-    if (STATS) { cn.nodes++; cn.it_inner++; }
-    const QAxis X = {a.w * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
-    const QAxis Y = {b.x * inv.y, __builtin_fmaf(a.y, inv.y, -oi.y)};
-    const QAxis Z = {b.y * inv.z, __builtin_fmaf(a.z, inv.z, -oi.z)};
-    // plane words (children 0-3 | 4-7), swapped into near / far order by the sign of 1/d
-    const uint32_t lx[2] = {__float_as_uint(b.z), __float_as_uint(b.w)}, hx[2] = {__float_as_uint(c.x), __float_as_uint(c.y)};
-    const uint32_t ly[2] = {__float_as_uint(c.z), __float_as_uint(c.w)}, hy[2] = {__float_as_uint(e.x), __float_as_uint(e.y)};
-    const uint32_t lz[2] = {__float_as_uint(e.z), __float_as_uint(e.w)}, hz[2] = {__float_as_uint(g.x), __float_as_uint(g.y)};
-    const int r[8] = {__float_as_int(ra.x), __float_as_int(ra.y), __float_as_int(ra.z), __float_as_int(ra.w),
-                      __float_as_int(rb.x), __float_as_int(rb.y), __float_as_int(rb.z), __float_as_int(rb.w)};
-    bool h[8];
-    float t[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int w = k >> 2;
-        h[k] = qchild(k & 3, sx ? hx[w] : lx[w], sx ? lx[w] : hx[w], sy ? hy[w] : ly[w], sy ? ly[w] : hy[w],
-                      sz ? hz[w] : lz[w], sz ? lz[w] : hz[w], X, Y, Z, tmin, best, t[k]) &&
-               r[k] != kSentinel;
-    }
-    int nxt = -1;   // slot visited next
-    if (MODE == 2) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) nxt = h[k] ? k : nxt;
-    } else {
-        float tb = INFINITY;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const bool lt = h[k] && t[k] < tb;
-            tb = lt ? t[k] : tb;
-            nxt = lt ? k : nxt;
-        }
-    }
-    auto step = [&](auto st) {
-        int rn = kSentinel;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const bool push = h[k] && k != nxt;
-            rn = k == nxt ? r[k] : rn;
-            st.put(sp + 1, r[k]);
-            sp += push ? 1 : 0;
-        }
-        const int top = st.get(sp);
-        cur = nxt >= 0 ? rn : top;
-        sp -= nxt >= 0 ? 0 : 1;
-    };
-    if (stk.lds_only(sp + 8)) step(stk.lds());
-    else step(stk);
-}
-
-template <bool STATS, int MODE, class S, bool QN = false, bool RES = false, bool W8 = false>
+template <bool STATS, int MODE, class S, bool QN = false, bool RES = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
                                              float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0,
@@ -564,8 +506,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     int leaf = ts.leaf;
     do {
         while (cur >= 0 && cur != kSentinel) {
-            if (W8) visit_node8q<STATS, MODE, S>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn);
-            else visit_node4<STATS, MODE, S, QN>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn);
+            visit_node4<STATS, MODE, S, QN>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn);
             if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
@@ -623,140 +564,6 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
         tsp->cur = cur; tsp->leaf = leaf; tsp->sp = sp; tsp->best_id = best_id; tsp->best = best;
         return !(cur != kSentinel || leaf < 0);
     }
-    return best_id >= 0;
-}
-
-// ------------------------------------------------ spread leaf phase (SPREAD variants)
-// In the while-while leaf phase only the lanes holding a leaf test triangles, each its
-// own leaf's 1-4 triangles in sequence (31 % SIMD efficiency at C2).  Here
-// one leaf "trip" spreads every (lane, triangle) pair of the wave over all 64 lanes,
-// idle and finished lanes included: pair p = prefix(count) + k is tested by lane
-// p mod 64 with the owner's ray, bound and id (ds_bpermute), and the owner's closest
-// (t, id) is reduced with a 64-bit LDS atomic min of (t bits << 32 | id).  Every pair
-// is tested against the owner's (t, id) from before the trip, with the same strict
-// t_min < t < best test and id tie rule as sequential testing, so the minimum over
-// the accepted pairs is exactly the sequential result (t > t_min > 0: the bit
-// patterns of the candidate t order like the floats).  Any-hit lanes test every
-// triangle of their leaf (the first hit no longer stops the leaf: the boolean result
-// is the same).  Per wave: 256 owner bytes (leaves of <= 4 triangles, 64 lanes) and
-// 64 result words in LDS.
-struct SpreadLds {
-    unsigned long long* res;   // this wave's 64 result words
-    uint8_t* own;              // this wave's 256 pair -> owner lane entries
-};
-constexpr int kSpreadBytesPerWave = 64 * 8 + 256;
-
-__device__ __forceinline__ unsigned long long pack_hit(float t, int id) {
-    return ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)id;
-}
-
-template <bool STATS, int MODE, class S>
-__device__ __forceinline__ void spread_leaf_trip(const float4* __restrict__ tris, V3 o, V3 d, float tmin, bool any,
-                                                 float& best, int& best_id, int& leaf, int& cur, int& sp, S stk,
-                                                 SpreadLds sl, int lane, Counters& cn) {
-    const bool hl = leaf < 0;
-    const int v = -leaf - 1;
-    const int cnt = hl ? (v & 7) + 1 : 0;   // <= 4 (host: spread variants need leaves of <= 4 triangles)
-    uint32_t pre = 0, total = 0;
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-        const uint64_t m = __ballot((cnt >> b) & 1);
-        pre += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
-        total += (uint32_t)__popcll(m) << b;
-    }
-    for (int k = 0; __ballot(k < cnt); ++k)
-        if (k < cnt) sl.own[pre + k] = (uint8_t)lane;
-    if (hl) sl.res[lane] = pack_hit(best, best_id);
-    const int rel = (v >> 3) - (int)pre;    // owner's first triangle minus its first pair index
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t base = 0; base < total; base += 64) {
-        const uint32_t p = base + (uint32_t)lane;
-        const bool act = p < total;
-        const int ow = act ? (int)sl.own[p] : lane;
-        const V3 oo = v3(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
-        const V3 od = v3(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
-        const float ob = __shfl(best, ow);
-        const int obid = __shfl(best_id, ow);
-        const int orel = __shfl(rel, ow);
-        const bool oany = MODE == 0 ? __shfl((int)any, ow) != 0 : any;
-        if (act) {
-            const float4* tp = tris + (size_t)(orel + (int)p) * 3;
-            const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
-            const int id = __float_as_int(q0.w);
-            float t;
-            if (STATS) cn.tris++;
-            if (mt_u(xyz(q0), xyz(q1), xyz(q2), oo, od, tmin, ob, id, obid, oany, t))
-                atomicMin(&sl.res[ow], pack_hit(t, id));
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (hl) {
-        if (STATS) cn.it_leaf++;
-        const unsigned long long r = sl.res[lane];
-        best = __uint_as_float((uint32_t)(r >> 32));
-        best_id = (int)(uint32_t)r;
-        if (any && best_id >= 0) {
-            leaf = 0;
-            cur = kSentinel;
-        } else {
-            leaf = cur;
-            if (cur < 0) {
-                cur = stk.get(sp);
-                --sp;
-            }
-        }
-    }
-}
-
-// While-while BVH4 traversal with the spread leaf phase.  Called by EVERY lane of the wave
-// (the leaf trips need all 64 as workers): lanes with `part` false only work for others.
-template <bool STATS, int MODE, class S, bool QN>
-__device__ __forceinline__ bool traverse_sp(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                            V3 d, float tmin, float tmax, bool any_lane, bool part, S stk, SpreadLds sl,
-                                            int& hit_id, float& hit_t, Counters& cn, int* fault, int leaf_break,
-                                            int leaf_exit, uint32_t guard_lim) {
-    const bool any = MODE == 0 ? any_lane : MODE == 2;
-    const int lane = (int)__lane_id();
-    const V3 inv = ray_inv(d);
-    V3 oi = o * inv;
-    const int sx = __float_as_int(inv.x) < 0 ? 1 : 0, sy = __float_as_int(inv.y) < 0 ? 1 : 0,
-              sz = __float_as_int(inv.z) < 0 ? 1 : 0;
-    stk.put(0, kSentinel);
-    float best = tmax;
-    int best_id = -1;
-    int sp = 0;
-    int cur = part ? root_for(tmax) : kSentinel;
-    int leaf = 0;
-    uint32_t guard = 0;
-    while (__ballot(cur != kSentinel || leaf < 0)) {
-        while (cur >= 0 && cur != kSentinel) {
-            visit_node4<STATS, MODE, S, QN>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn);
-            if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
-            if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
-                leaf = cur;
-                cur = stk.get(sp);
-                --sp;
-            }
-            if (__popcll(__ballot(leaf >= 0)) <= (uint32_t)leaf_break) break;
-        }
-        if (__ballot(leaf < 0)) {
-            do {
-                spread_leaf_trip<STATS, MODE, S>(tris, o, d, tmin, any, best, best_id, leaf, cur, sp, stk, sl, lane, cn);
-            } while (__popcll(__ballot(leaf < 0)) > (uint32_t)leaf_exit);
-        }
-        // watchdog (see traverse_ww4)
-        if ((cur != kSentinel || leaf < 0) && ++guard > guard_lim) {
-            if (fault) atomicOr(fault, 1);
-            cur = kSentinel;
-            leaf = 0;
-        }
-    }
-    hit_id = best_id;
-    hit_t = best;
     return best_id >= 0;
 }
 
@@ -856,11 +663,6 @@ void trace_kernel(TraceParams P) {
     constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
     constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
     constexpr bool MIS = (VAR & 256) != 0;     // MIS direct lighting (sample_direct_lighting2) instead of NEE
-    constexpr bool SPREAD = (VAR & 512) != 0;  // spread leaf phase (traverse_sp); not with RESUME
-    constexpr bool W8 = (VAR & 1024) != 0;     // quantised BVH8 nodes (visit_node8q); with QNODE, not SPREAD
-    static_assert(!W8 || (QNODE && !SPREAD), "BVH8 nodes are quantised and traversed by traverse_ww4");
-    static_assert(!(SPREAD && RESUME), "the spread leaf phase needs every lane in the traversal");
-    constexpr int kSpreadF4 = SPREAD ? kSpreadBytesPerWave * (kBlock / 64) / 16 : 0;
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
     int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
@@ -881,7 +683,7 @@ void trace_kernel(TraceParams P) {
     if (SCENE_LDS) {
         // small scene: copy BVH + triangles, and the shading data (normals, frames,
         // materials, emitters), into LDS once per persistent block
-        float4* sn = smem + kStackWords * kBlock / 4 + kSpreadF4;
+        float4* sn = smem + kStackWords * kBlock / 4;
         float4* st4 = sn + P.n_node_f4;
         float4* snm = st4 + P.n_tri_f4;
         float4* sfr = snm + P.n_tri;
@@ -1018,22 +820,20 @@ void trace_kernel(TraceParams P) {
             if (exhausted && q_next == q_end) break;
             continue;
         }
-        // lanes with a query of this iteration's kind; the spread variants keep the others in
-        // the traversal call as leaf-phase workers
-        const bool part = item >= 0 && !(PHASE && (qtype == Q_SHADOW) != do_shadow);
-        if (!SPREAD && !part) continue;
+        if (item < 0) continue;
+        if (PHASE && (qtype == Q_SHADOW) != do_shadow) continue;
 
         // ------------------------------------------------------- one query
         int hid = -1;
         float ht = 0.0f;
         bool hit;
         if (STATS) {
-            if (part && !pending) {
+            if (!pending) {
                 if (qtype == Q_EXT) cn.ext++; else cn.shadow++;
             }
             // wave-level clocks: the first active lane books the interval
             const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
-            const uint64_t active = __ballot(part);
+            const uint64_t active = __ballot(true);
             t_b = __builtin_amdgcn_s_memtime();
             if (leader) {
                 c_refill += t_b - t_a;
@@ -1047,22 +847,7 @@ void trace_kernel(TraceParams P) {
         const int lb = exhausted ? 0 : P.leaf_break, le = exhausted ? 0 : P.leaf_exit;
         const uint32_t glim = P.guard_trips;
         if (STATS && !pending) cn.q0 = cn.nodes;   // node visits at the start of this query
-        if (SPREAD) {
-            char* sb = reinterpret_cast<char*>(smem) + kStackWords * kBlock * 4;
-            const int w = threadIdx.x >> 6;
-            const SpreadLds sl = {reinterpret_cast<unsigned long long*>(sb) + 64 * w,
-                                  reinterpret_cast<uint8_t*>(sb + 512 * (kBlock / 64)) + 256 * w};
-            if (PHASE && do_shadow)
-                hit = traverse_sp<STATS, 2, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, true, part, stk, sl, hid,
-                                                           ht, cn, P.fault, lb, le, glim);
-            else if (PHASE)
-                hit = traverse_sp<STATS, 1, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, false, part, stk, sl,
-                                                           hid, ht, cn, P.fault, lb, le, glim);
-            else
-                hit = traverse_sp<STATS, 0, StackT, QNODE>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW, part,
-                                                           stk, sl, hid, ht, cn, P.fault, lb, le, glim);
-            if (!part) continue;
-        } else if (RESUME) {
+        if (RESUME) {
             if (!pending) tstate_init(tst, stk, tmax);
             // suspending a query only pays while idle lanes can be refilled: once the work
             // queue is exhausted (the launch's drain) the wave keeps traversing instead of
@@ -1070,13 +855,13 @@ void trace_kernel(TraceParams P) {
             const int res_min = exhausted ? 0 : P.resume_min;
             bool done;
             if (PHASE && do_shadow)
-                done = traverse_ww4<STATS, 2, StackT, QNODE, true, W8>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
                                                                   ht, cn, &tst, res_min, P.fault, lb, le, glim);
             else if (PHASE)
-                done = traverse_ww4<STATS, 1, StackT, QNODE, true, W8>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
                                                                   ht, cn, &tst, res_min, P.fault, lb, le, glim);
             else
-                done = traverse_ww4<STATS, 0, StackT, QNODE, true, W8>(g_nodes, g_tris, o, d, kTMin, tmax,
+                done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax,
                                                                   qtype == Q_SHADOW, stk, hid, ht, cn, &tst, res_min,
                                                                   P.fault, lb, le, glim);
             pending = !done;
@@ -1084,13 +869,13 @@ void trace_kernel(TraceParams P) {
             hit = hid >= 0;
         } else if (PHASE) {
             if (do_shadow)
-                hit = traverse_ww4<STATS, 2, StackT, QNODE, false, W8>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
                                                                   ht, cn, nullptr, 0, P.fault, lb, le, glim);
             else
-                hit = traverse_ww4<STATS, 1, StackT, QNODE, false, W8>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
                                                                   ht, cn, nullptr, 0, P.fault, lb, le, glim);
         } else {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false, W8>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
                                                               stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim);
         }
 
@@ -1417,10 +1202,7 @@ void trace_kernel(TraceParams P) {
     X(kVarLdsAnyOcc, 8, true, 1)              \
     X(kVarGlobal, 224, false, 6)              \
     X(kVarLdsMis, 256, true, 6)               \
-    X(kVarGlobalMis, 480, false, 6)           \
-    X(kVarLdsSpread, 520, true, 6)            \
-    X(kVarGlobalSpread, 608, false, 6)        \
-    X(kVarGlobal8, 1248, false, 6)
+    X(kVarGlobalMis, 480, false, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>

@@ -62,23 +62,6 @@ void collapse_bvh4(const BvhHost& b2, Bvh4Host* out);
 constexpr int kNodeQF4 = 4;
 void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out);
 
-// Quantised BVH8 for scenes read from HBM: one node = 8 x float4 = 128 B (one cache line):
-//   f[0] = (origin.x, origin.y, origin.z, s.x)
-//   f[1] = (s.y, s.z, qlo.x[0..3], qlo.x[4..7])     q = u8 grid coordinate per child
-//   f[2] = (qhi.x[0..3], qhi.x[4..7], qlo.y[0..3], qlo.y[4..7])
-//   f[3] = (qhi.y[0..3], qhi.y[4..7], qlo.z[0..3], qlo.z[4..7])
-//   f[4] = (qhi.z[0..3], qhi.z[4..7], 0, 0)
-//   f[5], f[6] = child refs 0..3, 4..7 (as Bvh4Host; empty slots 0x7FFFFFFF); f[7] unused
-// Collapsed from the BVH2 like the BVH4 (largest-area inner child opened first).
-constexpr int kNode8F4 = 8;
-struct Bvh8Host {
-    std::vector<float> nodes;      // n_nodes * 32
-    int64_t n_nodes = 0;
-    int32_t depth = 0;
-    int32_t stack_need = 0;        // worst case: 7 pushes per level + sentinel
-};
-void build_bvh8q(const BvhHost& b2, float pad, Bvh8Host* out);
-
 // Builds a binned-SAH BVH2 over triangles (tri_v: n x 9 f32 world vertices).
 // Box padding keeps the slab test conservative w.r.t. Moller-Trumbore's own
 // rounding so traversal returns exactly the brute-force closest hit.

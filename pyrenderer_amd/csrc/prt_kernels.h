@@ -60,19 +60,11 @@ constexpr int kVarGlobal = 3;      // global scene: quantised 64-B nodes, LDS st
 // estimator variants: the reference's unused MIS direct lighting (PRT_FLAG_MIS_NEE)
 constexpr int kVarLdsMis = 4;      // LDS scene, mixed schedule, >= 6 waves/SIMD
 constexpr int kVarGlobalMis = 5;   // kVarGlobal + MIS
-// spread leaf phase (prt_device.h traverse_sp): every (lane, triangle) pair of a leaf trip
-// spread over all 64 lanes; leaves of <= 4 triangles
-constexpr int kVarLdsSpread = 6;     // kVarLds + spread leaf phase
-constexpr int kVarGlobalSpread = 7;  // global scene (quantised nodes, spill stack, mixed schedule) + spread
-// quantised BVH8 (one 128-B line per node, 8 child boxes per fetch): global scenes
-constexpr int kVarGlobal8 = 8;       // kVarGlobal over the BVH8
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 8;
+constexpr int kVarLast = 5;
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
-bool variant_spreads(int var);
-bool variant_wide8(int var);
 bool variant_quantized(int var);
 
 int stack_variant(int bvh_depth);

@@ -132,7 +132,6 @@ size_t lds_scene_bytes(const TraceParams& P) {
 
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
     size_t b = (size_t)stack * kBlock * sizeof(int);
-    if (variant_spreads(var)) b += (size_t)kSpreadBytesPerWave * (kBlock / 64);
     if (variant_uses_lds(var)) b += lds_scene_bytes(P);
     return b;
 }
@@ -204,24 +203,6 @@ bool variant_quantized(int var) {
 bool variant_spills(int var) {
     switch (var) {
 #define X(id, bits, lds, wpe) case id: return (bits & 32) != 0;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
-
-bool variant_wide8(int var) {
-    switch (var) {
-#define X(id, bits, lds, wpe) case id: return (bits & 1024) != 0;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
-
-bool variant_spreads(int var) {
-    switch (var) {
-#define X(id, bits, lds, wpe) case id: return (bits & 512) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;

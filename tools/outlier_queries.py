@@ -4,13 +4,13 @@ import bench
 from pyrenderer_amd._native import PRT_FLAG_STATS
 from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
 from pyrenderer_amd.flatten import flatten_scene
-cfg = bench.CONFIGS[4]
+cfg = bench.CONFIGS[int(sys.argv[1]) if len(sys.argv) > 1 else 4]
 scene, camera = bench.load_scene(cfg["scene"])
 flat = flatten_scene(scene)
 ds = DeviceScene(flat, 0)
 cam = camera.convert_to_taichi_camera().packed()
-ids = interleaved_tiles(512, 512, 64)
-ds.render_tiles(cam, 512, 512, 64, 64, ids, 64, 8, 0, PRT_FLAG_STATS)
+ids = interleaved_tiles(cfg["res"], cfg["res"], 64)
+ds.render_tiles(cam, cfg["res"], cfg["res"], 64, 64, ids, cfg["spp"], cfg["depth"], 0, PRT_FLAG_STATS)
 w = ds.diag_words(24 + 128)
 print("max_q", int(w[16]), "n_outliers", int(w[23]))
 for k in range(min(16, int(w[23]))):
