@@ -707,9 +707,10 @@ void trace_kernel(TraceParams P) {
         s_loff = slo;
     }
     const int lane = threadIdx.x & 63;
-    // diagnostic (P.wave_clock, env PRT_WAVE_CLOCK): each wave's start / end real time
-    const uint64_t t_start = P.wave_clock ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint32_t n_taken = 0;   // items this wave took from the queue (diagnostic)
+    // diagnostic (P.wave_clock, env PRT_WAVE_CLOCK): each wave's start / end real time and the
+    // items it took, kept in memory (not registers: the hot loop's VGPR budget is tight)
+    if (P.wave_clock && lane == 0)
+        P.wave_clock[3 * ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6))] = __builtin_amdgcn_s_memrealtime();
 
     // wave-uniform work queue [q_next, q_end)
     uint32_t q_next = 0, q_end = 0;
@@ -764,7 +765,8 @@ void trace_kernel(TraceParams P) {
                 } else {
                     q_next = base;
                     q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
-                    n_taken += q_end - q_next;
+                    if (P.wave_clock && lane == 0)
+                        P.wave_clock[3 * ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) + 2] += q_end - q_next;
                     // n_slots is a multiple of 64 (tile sizes are powers of two >= 64 px),
                     // so a chunk never straddles two samples: one scalar division per chunk
                     chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
@@ -1147,12 +1149,8 @@ void trace_kernel(TraceParams P) {
             if (leader) c_shade += __builtin_amdgcn_s_memtime() - t_a;
         }
     }
-    if (P.wave_clock && lane == 0) {
-        const size_t w = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-        P.wave_clock[3 * w] = t_start;
-        P.wave_clock[3 * w + 1] = __builtin_amdgcn_s_memrealtime();
-        P.wave_clock[3 * w + 2] = n_taken;
-    }
+    if (P.wave_clock && lane == 0)
+        P.wave_clock[3 * ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) + 1] = __builtin_amdgcn_s_memrealtime();
     if (STATS) {
         uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
         for (int off = 32; off > 0; off >>= 1) {
