@@ -64,22 +64,34 @@ __device__ __forceinline__ bool div_is_nan(float a, float b) {
 // is therefore bit-identical to the full expansion, and the reciprocal refinement is
 // shared by the three quotients of one denominator.  A wave with any lane outside the
 // range (zero, tiny, huge, inf, NaN) takes the plain divisions.
-__device__ __forceinline__ V3 div3(V3 a, float b) {
-    // fminf drops a NaN operand, the sum does not: a NaN or inf anywhere fails `sum <= 2^40`
+// fminf drops a NaN operand, the sum does not: a NaN or inf anywhere fails `sum <= 2^40`
+__device__ __forceinline__ bool div3_fast_ok(V3 a, float b) {
     const float lo = fminf(fminf(fabsf(a.x), fabsf(a.y)), fminf(fabsf(a.z), fabsf(b)));
     const float sum = (fabsf(a.x) + fabsf(a.y)) + (fabsf(a.z) + fabsf(b));
-    const bool ok = lo >= 0x1p-40f && sum <= 0x1p40f;
-    if (__ballot(!ok) == 0) {
-        float r = __builtin_amdgcn_rcpf(b);
-        r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
-        auto q1 = [&](float n) {
-            float q = n * r;
-            q = __builtin_fmaf(__builtin_fmaf(-b, q, n), r, q);
-            return __builtin_fmaf(__builtin_fmaf(-b, q, n), r, q);
-        };
-        return v3(q1(a.x), q1(a.y), q1(a.z));
-    }
+    return lo >= 0x1p-40f && sum <= 0x1p40f;
+}
+__device__ __forceinline__ V3 div3_fast(V3 a, float b) {
+    float r = __builtin_amdgcn_rcpf(b);
+    r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+    auto q1 = [&](float n) {
+        float q = n * r;
+        q = __builtin_fmaf(__builtin_fmaf(-b, q, n), r, q);
+        return __builtin_fmaf(__builtin_fmaf(-b, q, n), r, q);
+    };
+    return v3(q1(a.x), q1(a.y), q1(a.z));
+}
+__device__ __forceinline__ V3 div3(V3 a, float b) {
+    if (__ballot(!div3_fast_ok(a, b)) == 0) return div3_fast(a, b);
     return v3(a.x / b, a.y / b, a.z / b);
+}
+// (a.x / pdf, a.y / pdf, a.z / pdf) under the reference's NaN rule (tracing.py:146-148): when
+// any quotient would be NaN, pdf = 1e-4 instead.  Operands in div3's fast range (finite,
+// magnitudes in [2^-40, 2^40]) cannot give a NaN quotient, so a wave whose lanes are all in
+// range skips the NaN tests.
+__device__ __forceinline__ V3 div3_nan_guard(V3 a, float pdf) {
+    if (__ballot(!div3_fast_ok(a, pdf)) == 0) return div3_fast(a, pdf);
+    if (div_is_nan(a.x, pdf) || div_is_nan(a.y, pdf) || div_is_nan(a.z, pdf)) pdf = 1e-4f;
+    return v3(a.x / pdf, a.y / pdf, a.z / pdf);
 }
 // 1 / b, correctly rounded: for finite |b| in [2^-40, 2^40] the division expansion (see
 // div3) with numerator 1 is the refined reciprocal plus two quotient corrections
@@ -94,9 +106,32 @@ __device__ __forceinline__ float rcp_exact(float b) {
     }
     return 1.0f / b;
 }
+// Correctly rounded sqrt.  hipcc expands sqrtf on gfx950 as: scale x by 2^32 when
+// x < 2^-96, v_sqrt_f32, correct the result by one ulp down / up from the signs of the
+// residuals fma(-(s -/+ 1 ulp), s, x), unscale, and return x itself for +-0 / +inf.  For
+// finite x in [2^-96, FLT_MAX] the scaling and the class test change nothing, so with FAST
+// a wave whose lanes are all in that range runs the corrected v_sqrt alone (bit-identical);
+// other waves take sqrtf.  FAST is used by the LDS-scene kernels (C2 -0.5 %); the
+// global-scene kernel keeps sqrtf (its extra live registers cost spills there).
+template <bool FAST>
+__device__ __forceinline__ float sqrt_cr(float x) {
+    if constexpr (FAST) {
+        if (__ballot(!(x >= 0x1p-96f && x <= 0x1.fffffep127f)) == 0) {
+            const float s = __builtin_amdgcn_sqrtf(x);
+            const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+            const float su = __uint_as_float(__float_as_uint(s) + 1u);
+            const float rd = __builtin_fmaf(-sd, s, x);
+            const float ru = __builtin_fmaf(-su, s, x);
+            const float r = rd <= 0.0f ? sd : s;
+            return ru > 0.0f ? su : r;
+        }
+    }
+    return sqrtf(x);
+}
 // taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt)
+template <bool FAST = false>
 __device__ __forceinline__ V3 normalize(V3 a) {
-    return div3(a, sqrtf(dot(a, a)));
+    return div3(a, sqrt_cr<FAST>(dot(a, a)));
 }
 __device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
 
@@ -133,6 +168,7 @@ __device__ __forceinline__ float poly_cos(float x) {
     return ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z
            - 0.5f * z + 1.0f;
 }
+template <bool FAST = false>
 __device__ __forceinline__ V3 cosine_hemisphere(float u0, float u1) {
     float ox = 2.0f * u0 - 1.0f, oy = 2.0f * u1 - 1.0f;
     float dx = 0.0f, dy = 0.0f;
@@ -149,7 +185,7 @@ __device__ __forceinline__ V3 cosine_hemisphere(float u0, float u1) {
         dy = r * (wide ? ps : pc);
     }
     float m = 1.0f - dx * dx - dy * dy;
-    return v3(dx, dy, sqrtf(m > 0.0f ? m : 0.0f));
+    return v3(dx, dy, sqrt_cr<FAST>(m > 0.0f ? m : 0.0f));
 }
 
 // rotate_z_to + rotate_vector (mat4_taichi.py:9-60): rows (x, z, n)
@@ -283,17 +319,8 @@ constexpr int kSentinel = 0x7FFFFFFF;
 constexpr uint32_t kGuardTrips = 1u << 20;   // leaf batches per query before the watchdog trips
 
 // While-while over the BVH4 (prt_internal.h): one node fetch tests four child
-// boxes; hit children are ordered near-to-far with a 5-comparator network, the
-// nearest is visited next and the others pushed far-first.
-__device__ __forceinline__ void cswap(float& ta, int& ra, float& tb, int& rb) {
-    bool sw = tb < ta;
-    float t = sw ? tb : ta;
-    tb = sw ? ta : tb;
-    ta = t;
-    int r = sw ? rb : ra;
-    rb = sw ? ra : rb;
-    ra = r;
-}
+// boxes; the nearest hit child is visited next (a 3-comparator tournament) and the
+// other hit children are pushed.
 
 // Per-lane traversal stacks.  LdsStack: entry k at l[k * kBlock] (conflict-free).
 // SpillStack: the first LST entries in LDS, deeper ones in a per-lane global area
@@ -418,14 +445,17 @@ __device__ __forceinline__ V3 ray_inv(V3 d) {
 // Pushes write the slot above the top unconditionally and advance the stack pointer by
 // the hit predicate (no exec-mask branches); the highest slot written is the same as
 // with conditional pushes (<= 3 above the entry top).
-template <bool STATS, int MODE, class S, bool QN>
+template <bool STATS, int MODE, class S, bool QN, bool TOP = false>
 __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, int& cur, int& sp, S stk, V3 inv, V3 oi,
-                                            int sx, int sy, int sz, float tmin, float best, Counters& cn) {
+                                            int sx, int sy, int sz, float tmin, float best, Counters& cn,
+                                            const float4* top = nullptr, int n_top = 0) {
     float t0, t1, t2, t3;
     bool h0, h1, h2, h3;
     int r0, r1, r2, r3;
     if (QN) {
-        const float4* nd = nodes + (size_t)cur * 4;
+        // TOP: nodes [0, n_top) (the breadth-first top of the tree) are read from the block's
+        // LDS copy, the others from global memory (one flat load serves both)
+        const float4* nd = (TOP && cur < n_top ? top : nodes) + (size_t)cur * 4;
         float4 a = nd[0], b = nd[1], c = nd[2], rf = nd[3];
         if (STATS) { cn.nodes++; cn.it_inner++; }
         QAxis X = {a.w * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
@@ -462,33 +492,39 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
             cur = h3 ? r3 : top;
             sp -= h3 ? 0 : 1;
         } else {
-            t0 = h0 ? t0 : INFINITY;
-            t1 = h1 ? t1 : INFINITY;
-            t2 = h2 ? t2 : INFINITY;
-            t3 = h3 ? t3 : INFINITY;
-            int nh = (int)h0 + (int)h1 + (int)h2 + (int)h3;
-            // nearest hit child first (3 comparators); the other hits pushed in slot order
-            cswap(t0, r0, t1, r1);
-            cswap(t2, r2, t3, r3);
-            cswap(t0, r0, t2, r2);
-            st.put(sp + 1, r3); sp += t3 != INFINITY ? 1 : 0;
-            st.put(sp + 1, r2); sp += t2 != INFINITY ? 1 : 0;
-            st.put(sp + 1, r1); sp += t1 != INFINITY ? 1 : 0;
-            int top = st.get(sp);
-            cur = nh > 0 ? r0 : top;
-            sp -= nh > 0 ? 0 : 1;
+            // nearest hit child first by a 3-comparator tournament on the entry distances
+            // (misses count as +inf); the three others are pushed when hit: the loser of each
+            // pair is a hit iff both of the pair are, the loser of the final iff each pair
+            // has a hit
+            const float k0 = h0 ? t0 : INFINITY, k1 = h1 ? t1 : INFINITY;
+            const float k2 = h2 ? t2 : INFINITY, k3 = h3 ? t3 : INFINITY;
+            const bool m01 = k1 < k0, m23 = k3 < k2;
+            const float a = m01 ? k1 : k0, c = m23 ? k3 : k2;
+            const int ra = m01 ? r1 : r0, rb = m01 ? r0 : r1;
+            const int rc = m23 ? r3 : r2, rd = m23 ? r2 : r3;
+            const bool m = c < a;
+            const int rn = m ? rc : ra, rl = m ? ra : rc;
+            const bool p01 = h0 | h1, p23 = h2 | h3;
+            st.put(sp + 1, rb); sp += (h0 & h1) ? 1 : 0;
+            st.put(sp + 1, rd); sp += (h2 & h3) ? 1 : 0;
+            st.put(sp + 1, rl); sp += (p01 & p23) ? 1 : 0;
+            const int tp = st.get(sp);
+            const bool any_hit = p01 | p23;
+            cur = any_hit ? rn : tp;
+            sp -= any_hit ? 0 : 1;
         }
     };
     if (stk.lds_only(sp + 3)) step(stk.lds());
     else step(stk);
 }
 
-template <bool STATS, int MODE, class S, bool QN = false, bool RES = false>
+template <bool STATS, int MODE, class S, bool QN = false, bool RES = false, bool TOP = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
                                              float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0,
                                              int* fault = nullptr, int leaf_break = 0, int leaf_exit = 0,
-                                             uint32_t guard_lim = kGuardTrips) {
+                                             uint32_t guard_lim = kGuardTrips, const float4* top = nullptr,
+                                             int n_top = 0) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     const V3 inv = ray_inv(d);
     V3 oi = o * inv;
@@ -506,7 +542,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     int leaf = ts.leaf;
     do {
         while (cur >= 0 && cur != kSentinel) {
-            visit_node4<STATS, MODE, S, QN>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn);
+            visit_node4<STATS, MODE, S, QN, TOP>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn, top, n_top);
             if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
@@ -663,6 +699,8 @@ void trace_kernel(TraceParams P) {
     constexpr bool QNODE = (VAR & 64) != 0;    // quantised 64-B BVH4 nodes
     constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
     constexpr bool MIS = (VAR & 256) != 0;     // MIS direct lighting (sample_direct_lighting2) instead of NEE
+    constexpr bool FSQ = SCENE_LDS;            // shading sqrt fast path (sqrt_cr)
+    constexpr bool TOPN = (VAR & 512) != 0;    // quantised nodes [0, n_top) in LDS
     extern __shared__ float4 smem[];
     constexpr int kStackWords = STACK;
     int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
@@ -705,6 +743,17 @@ void trace_kernel(TraceParams P) {
         s_mats = reinterpret_cast<const float*>(smt);
         s_lv = slv;
         s_loff = slo;
+    }
+    const float4* g_top = nullptr;
+    int n_top = 0;
+    if constexpr (TOPN) {
+        // the breadth-first top of the tree (collapse_bvh4 numbers it first), once per block
+        float4* st4 = smem + kStackWords * kBlock / 4;
+        for (int i = threadIdx.x; i < 4 * P.n_top; i += kBlock) st4[i] = P.nodes[i];
+        __syncthreads();
+        g_top = st4;
+        n_top = P.n_top;
+        asm volatile("" : "+s"(n_top));
     }
     const int lane = threadIdx.x & 63;
     // diagnostic (P.wave_clock, env PRT_WAVE_CLOCK): each wave's start / end real time and the
@@ -857,28 +906,28 @@ void trace_kernel(TraceParams P) {
             const int res_min = exhausted ? 0 : P.resume_min;
             bool done;
             if (PHASE && do_shadow)
-                done = traverse_ww4<STATS, 2, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
-                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
+                done = traverse_ww4<STATS, 2, StackT, QNODE, true, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim, g_top, n_top);
             else if (PHASE)
-                done = traverse_ww4<STATS, 1, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
-                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
+                done = traverse_ww4<STATS, 1, StackT, QNODE, true, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim, g_top, n_top);
             else
-                done = traverse_ww4<STATS, 0, StackT, QNODE, true>(g_nodes, g_tris, o, d, kTMin, tmax,
+                done = traverse_ww4<STATS, 0, StackT, QNODE, true, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax,
                                                                   qtype == Q_SHADOW, stk, hid, ht, cn, &tst, res_min,
-                                                                  P.fault, lb, le, glim);
+                                                                  P.fault, lb, le, glim, g_top, n_top);
             pending = !done;
             if (pending) continue;   // resume next iteration; no shading yet
             hit = hid >= 0;
         } else if (PHASE) {
             if (do_shadow)
-                hit = traverse_ww4<STATS, 2, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
-                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
+                hit = traverse_ww4<STATS, 2, StackT, QNODE, false, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim, g_top, n_top);
             else
-                hit = traverse_ww4<STATS, 1, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
-                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
+                hit = traverse_ww4<STATS, 1, StackT, QNODE, false, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim, g_top, n_top);
         } else {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
-                                                              stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
+                                                              stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim, g_top, n_top);
         }
 
         if (STATS) {
@@ -989,11 +1038,11 @@ void trace_kernel(TraceParams P) {
                     // same f32 arithmetic (per face and side); spheres build them here.
                     float u0 = rng_next(st);
                     float u1 = rng_next(st);
-                    V3 l = cosine_hemisphere(u0, u1);
+                    V3 l = cosine_hemisphere<FSQ>(u0, u1);
                     const float4* fr = s_fr + ((size_t)(hid < P.n_tri ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
                     if (hid < P.n_tri) {
                         float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
-                        wi = normalize(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
+                        wi = normalize<FSQ>(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
                     } else {
                         wi = to_world(n, l);
                     }
@@ -1005,15 +1054,14 @@ void trace_kernel(TraceParams P) {
                     // reference recomputes it with pdf = 1e-4.  (a / pdf) * InvPi is NaN
                     // exactly when a / pdf is, so the condition is decided before dividing.
                     V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                    if (div_is_nan(ad.x, pdf) || div_is_nan(ad.y, pdf) || div_is_nan(ad.z, pdf)) pdf = 1e-4f;
-                    V3 adp = div3(ad, pdf);
+                    V3 adp = div3_nan_guard(ad, pdf);
                     V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
                     beta = beta * nb;
                     // sample_direct_lighting (tracing.py:92-108)
                     int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
                     int lo = s_loff[li];
                     int f = rng_int(st, 0, s_loff[li + 1] - lo - 1);
-                    float su = sqrtf(rng_next(st));
+                    float su = sqrt_cr<FSQ>(rng_next(st));
                     float sv = rng_next(st);
                     float a = su * (1.0f - sv);
                     float b = su * sv;
@@ -1027,13 +1075,13 @@ void trace_kernel(TraceParams P) {
                         // (queries draw nothing, so the stream order is the reference's)
                         const float* em = s_mats + 8 * __float_as_int(LN.w);
                         mis_fl = v3(m[0] * kInvPi * em[0], m[1] * kInvPi * em[1], m[2] * kInvPi * em[2]);
-                        V3 tl = normalize(p2 - p);
+                        V3 tl = normalize<FSQ>(p2 - p);
                         float b0 = rng_next(st);
                         float b1 = rng_next(st);
-                        V3 bl = cosine_hemisphere(b0, b1);
+                        V3 bl = cosine_hemisphere<FSQ>(b0, b1);
                         if (hid < P.n_tri) {
                             float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
-                            mis_bd = normalize(xyz(f0) * bl.x + xyz(f1) * bl.y + xyz(f2) * bl.z);
+                            mis_bd = normalize<FSQ>(xyz(f0) * bl.x + xyz(f1) * bl.y + xyz(f2) * bl.z);
                         } else {
                             mis_bd = to_world(n, bl);
                         }
@@ -1057,7 +1105,7 @@ void trace_kernel(TraceParams P) {
                             tmax = kTMax;
                         }
                     } else {
-                    V3 w = normalize(p2 - p);
+                    V3 w = normalize<FSQ>(p2 - p);
                     float t_at = (p2.x - p.x) / w.x;
                     // w2 = normalize(p - p2) is -w bit for bit (round-to-nearest is sign
                     // symmetric) up to the sign of zero components, so dot(n2, w2) =
@@ -1200,7 +1248,8 @@ void trace_kernel(TraceParams P) {
     X(kVarLdsAnyOcc, 8, true, 1)              \
     X(kVarGlobal, 224, false, 6)              \
     X(kVarLdsMis, 256, true, 6)               \
-    X(kVarGlobalMis, 480, false, 6)
+    X(kVarGlobalMis, 480, false, 6)           \
+    X(kVarGlobalTop, 736, false, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>

@@ -133,6 +133,7 @@ size_t lds_scene_bytes(const TraceParams& P) {
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
     size_t b = (size_t)stack * kBlock * sizeof(int);
     if (variant_uses_lds(var)) b += lds_scene_bytes(P);
+    if (variant_top(var)) b += 64 * (size_t)P.n_top;
     return b;
 }
 
@@ -194,6 +195,15 @@ bool variant_mis(int var) {
 bool variant_quantized(int var) {
     switch (var) {
 #define X(id, bits, lds, wpe) case id: return (bits & 64) != 0;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
+bool variant_top(int var) {
+    switch (var) {
+#define X(id, bits, lds, wpe) case id: return (bits & 512) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;
