@@ -22,9 +22,8 @@ VAR_LDS = 1           # LDS-resident scene, phase-aligned schedule, >= 6 waves/S
 VAR_LDS_ANY_OCC = 2   # ... without the occupancy target
 VAR_GLOBAL = 3        # scene in HBM: quantised BVH4, LDS stack + global spill, suspended tails
 VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
-VAR_GLOBAL_TOP = 6    # VAR_GLOBAL + the breadth-first top of the BVH4 in LDS
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_GLOBAL_TOP)
-VAR_LAST = 6
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL)
+VAR_LAST = 5
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 

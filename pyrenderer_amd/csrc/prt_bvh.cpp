@@ -433,44 +433,6 @@ inline double child_area(const Child& c) {
 
 }  // namespace
 
-// Renumbers the BVH4 so that its first min(k, n) nodes in breadth-first order come first
-// (the root stays node 0) and the others keep their relative order: the kernels that keep
-// the top of the tree in LDS then test `node < n_top` (prt_device.h visit_node4).
-static void bfs_prefix_first(Bvh4Host* b4, int64_t k) {
-    const int64_t n = b4->n_nodes;
-    k = std::min(k, n);
-    std::vector<int64_t> bfs;
-    bfs.reserve((size_t)k);
-    std::vector<char> top((size_t)n, 0);
-    bfs.push_back(0);
-    top[0] = 1;
-    for (size_t h = 0; h < bfs.size() && (int64_t)bfs.size() < k; ++h) {
-        const float* f = b4->nodes.data() + (size_t)bfs[h] * 32;
-        for (int c = 0; c < 4 && (int64_t)bfs.size() < k; ++c) {
-            int32_t r;
-            std::memcpy(&r, f + 24 + c, 4);
-            if (r >= 0 && r != 0x7FFFFFFF) { bfs.push_back(r); top[(size_t)r] = 1; }
-        }
-    }
-    std::vector<int32_t> remap((size_t)n);
-    int64_t next = 0;
-    for (int64_t v : bfs) remap[(size_t)v] = (int32_t)next++;
-    for (int64_t v = 0; v < n; ++v)
-        if (!top[(size_t)v]) remap[(size_t)v] = (int32_t)next++;
-    std::vector<float> nodes(b4->nodes.size());
-    for (int64_t v = 0; v < n; ++v) {
-        float* f = nodes.data() + (size_t)remap[(size_t)v] * 32;
-        std::memcpy(f, b4->nodes.data() + (size_t)v * 32, 32 * sizeof(float));
-        for (int c = 0; c < 4; ++c) {
-            int32_t r;
-            std::memcpy(&r, f + 24 + c, 4);
-            if (r >= 0 && r != 0x7FFFFFFF) r = remap[(size_t)r];
-            std::memcpy(f + 24 + c, &r, 4);
-        }
-    }
-    b4->nodes.swap(nodes);
-}
-
 void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
     // Each BVH4 node takes a BVH2 node's two children and repeatedly opens the
     // inner child with the largest surface area until it holds four children.
@@ -529,7 +491,6 @@ void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
         out->depth = std::max(out->depth, it.depth);
     }
     out->stack_need = 3 * (out->depth + 1) + 1;
-    bfs_prefix_first(out, kTopNodesMax);
 }
 
 void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out) {

@@ -122,7 +122,6 @@ struct Scene {
     int resume_min = 32;             // resume variants (env PRT_RESUME_MIN; C4 after the r02 BVH fixes: 16 / 24 / 32 / 40 / 48 -> 19.4 / 19.1 / 19.0 / 19.4 / 19.8 ms)
     uint32_t guard_trips = 1u << 20; // traversal phases per query before the watchdog trips (env PRT_GUARD_TRIPS)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
-    int top_nodes = 128;             // top-level variants: quantised nodes kept in LDS (env PRT_LDS_TOP, <= kTopNodesMax)
     std::string wave_clock_path;     // env PRT_WAVE_CLOCK: append each trace launch's per-wave clocks here
     int64_t n_sph = 0;
     DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
@@ -239,11 +238,14 @@ void scene_sizes(const Scene* s, prt::TraceParams& P) {
     P.n_lt = s->n_lt;
     P.n_light = s->n_light;
 }
+// ... and whose node indices and leaf references fit the LDS kernels' 16-bit stack entries
+// (inner nodes < 0x7FFF, the sentinel; leaf refs >= -32768)
 bool lds_fits4(const Scene* s) {
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
     scene_sizes(s, P);
-    return (int64_t)prt::lds_scene_bytes(P) <= kLdsSceneBytes;
+    const int64_t n_refs = s->n_tri_f4 / 3;
+    return (int64_t)prt::lds_scene_bytes(P) <= kLdsSceneBytes && s->n_node4_f4 / 8 < 0x7FFF && n_refs * 8 <= 32768;
 }
 // LDS-resident scene when it fits; the >= 6 waves/SIMD build when six blocks' LDS
 // still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
@@ -365,7 +367,6 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         P.nodes = (const float4*)s->nodes4q.p;
         P.n_node_f4 = (int)s->n_node4q_f4;
     }
-    if (prt::variant_top(var)) P.n_top = (int)std::min<int64_t>(s->top_nodes, s->n_node4q_f4 / 4);
     if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
     // while-while leaf-phase entry: LDS scenes wait for every descending lane's leaf (their
     // leaves are cheap and traversals short); global scenes enter the leaf phase once at
@@ -660,8 +661,6 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         if (const char* gt = std::getenv("PRT_GUARD_TRIPS"))
             s->guard_trips = (uint32_t)std::max(1LL, std::min((long long)UINT32_MAX, std::atoll(gt)));
         if (const char* rm = std::getenv("PRT_RESUME_MIN")) s->resume_min = std::max(1, std::min(64, std::atoi(rm)));
-        if (const char* lt = std::getenv("PRT_LDS_TOP"))
-            s->top_nodes = (int)std::max<int64_t>(0, std::min<int64_t>(prt::kTopNodesMax, std::atoll(lt)));
         if (const char* sl = std::getenv("PRT_SPILL_LDS")) {
             int v = std::atoi(sl);
             s->spill_lds = v == 4 ? 4 : v == 32 ? 32 : 16;

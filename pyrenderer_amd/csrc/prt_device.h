@@ -328,6 +328,7 @@ constexpr uint32_t kGuardTrips = 1u << 20;   // leaf batches per query before th
 // the 1 M-triangle scene against a worst-case bound of 46), so a small LDS stack keeps
 // occupancy and the spill branch is almost never taken.
 struct LdsStack {
+    static constexpr int kSent = kSentinel;
     int* l;
     __device__ __forceinline__ void put(int k, int v) { l[k * kBlock] = v; }
     __device__ __forceinline__ int get(int k) const { return l[k * kBlock]; }
@@ -337,6 +338,7 @@ struct LdsStack {
 };
 template <int LST>
 struct SpillStack {
+    static constexpr int kSent = kSentinel;
     int* l;
     int* g;
     uint32_t gs;
@@ -354,6 +356,20 @@ struct SpillStack {
 #endif
     }
     __device__ __forceinline__ LdsStack lds() const { return LdsStack{l}; }
+};
+// LDS-resident scenes: 16-bit entries (half the stack's LDS, so the octant node copies
+// fit beside it at six blocks per CU).  Node indices and leaf references of such scenes fit
+// 16 bits (host check in lds_fits4), and the traversal sentinel is 0x7FFF: the block's LDS
+// copy of the BVH4 rewrites the empty-slot references to it.  Entry k of lane j sits at
+// 2 * (k * kBlock + (j & ~63) + 2 * (j & 31) + (j >> 5 & 1)): a half-wave's 32 lanes use 32
+// different banks.
+struct LdsStack16 {
+    static constexpr int kSent = 0x7FFF;
+    short* l;
+    __device__ __forceinline__ void put(int k, int v) { l[k * kBlock] = (short)v; }
+    __device__ __forceinline__ int get(int k) const { return (int)l[k * kBlock]; }
+    __device__ __forceinline__ bool lds_only(int) const { return true; }
+    __device__ __forceinline__ LdsStack16 lds() const { return *this; }
 };
 
 // MODE 0: per-lane query kind (`any` may differ between lanes); 1: every lane
@@ -393,12 +409,13 @@ struct TState { int cur, leaf, sp, best_id; float best; };
 // either (fminf drops the NaN), so traversing would walk every box along the whole line
 // (config 4: ~2000 node visits, the launch's last 2 ms); it starts finished instead, with
 // the same (miss) result.  Spheres still see the NaN bound (hit_sphere accepts it).
-__device__ __forceinline__ int root_for(float tmax) { return tmax == tmax ? 0 : kSentinel; }
+template <class S>
+__device__ __forceinline__ int root_for(float tmax) { return tmax == tmax ? 0 : S::kSent; }
 
 template <class S>
 __device__ __forceinline__ void tstate_init(TState& ts, S stk, float tmax) {
-    stk.put(0, kSentinel);
-    ts.cur = root_for(tmax); ts.leaf = 0; ts.sp = 0; ts.best_id = -1; ts.best = tmax;
+    stk.put(0, S::kSent);
+    ts.cur = root_for<S>(tmax); ts.leaf = 0; ts.sp = 0; ts.best_id = -1; ts.best = tmax;
 }
 
 // RES: the wave leaves the traversal loop once fewer than `min_lanes` lanes are still
@@ -445,17 +462,18 @@ __device__ __forceinline__ V3 ray_inv(V3 d) {
 // Pushes write the slot above the top unconditionally and advance the stack pointer by
 // the hit predicate (no exec-mask branches); the highest slot written is the same as
 // with conditional pushes (<= 3 above the entry top).
-template <bool STATS, int MODE, class S, bool QN, bool TOP = false>
+// OCT (LDS-resident scenes): `nodes` is the block's octant copy of the BVH4 (8 copies of each
+// node, copy k with the near and far planes of each axis pre-arranged for the direction signs
+// k = sx | sy << 1 | sz << 2: 7 float4 = nx, fx, ny, fy, nz, fz, refs; node stride 56 float4)
+// and `sx` holds the query's copy offset 7 k: the seven reads need no per-plane addresses.
+template <bool STATS, int MODE, class S, bool QN, bool OCT = false>
 __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, int& cur, int& sp, S stk, V3 inv, V3 oi,
-                                            int sx, int sy, int sz, float tmin, float best, Counters& cn,
-                                            const float4* top = nullptr, int n_top = 0) {
+                                            int sx, int sy, int sz, float tmin, float best, Counters& cn) {
     float t0, t1, t2, t3;
     bool h0, h1, h2, h3;
     int r0, r1, r2, r3;
     if (QN) {
-        // TOP: nodes [0, n_top) (the breadth-first top of the tree) are read from the block's
-        // LDS copy, the others from global memory (one flat load serves both)
-        const float4* nd = (TOP && cur < n_top ? top : nodes) + (size_t)cur * 4;
+        const float4* nd = nodes + (size_t)cur * 4;
         float4 a = nd[0], b = nd[1], c = nd[2], rf = nd[3];
         if (STATS) { cn.nodes++; cn.it_inner++; }
         QAxis X = {a.w * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
@@ -470,10 +488,16 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
         h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && r2 != kSentinel;
         h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && r3 != kSentinel;
     } else {
-        // near/far planes picked by address (the node stores lo and hi per axis)
-        const float4* nd = nodes + (size_t)cur * 8;
-        float4 nx = nd[sx], fx = nd[1 - sx], ny = nd[2 + sy], fy = nd[3 - sy], nz = nd[4 + sz], fz = nd[5 - sz];
-        float4 rf = nd[6];
+        float4 nx, fx, ny, fy, nz, fz, rf;
+        if (OCT) {
+            const float4* nd = nodes + (uint32_t)cur * 56u + sx;
+            nx = nd[0]; fx = nd[1]; ny = nd[2]; fy = nd[3]; nz = nd[4]; fz = nd[5]; rf = nd[6];
+        } else {
+            // near/far planes picked by address (the node stores lo and hi per axis)
+            const float4* nd = nodes + (size_t)cur * 8;
+            nx = nd[sx]; fx = nd[1 - sx]; ny = nd[2 + sy]; fy = nd[3 - sy]; nz = nd[4 + sz]; fz = nd[5 - sz];
+            rf = nd[6];
+        }
         if (STATS) { cn.nodes++; cn.it_inner++; }
         h0 = slab_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, oi, inv, tmin, best, t0);
         h1 = slab_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, oi, inv, tmin, best, t1);
@@ -518,19 +542,19 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     else step(stk);
 }
 
-template <bool STATS, int MODE, class S, bool QN = false, bool RES = false, bool TOP = false>
+template <bool STATS, int MODE, class S, bool QN = false, bool RES = false, bool OCT = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
                                              float& hit_t, Counters& cn, TState* tsp = nullptr, int min_lanes = 0,
                                              int* fault = nullptr, int leaf_break = 0, int leaf_exit = 0,
-                                             uint32_t guard_lim = kGuardTrips, const float4* top = nullptr,
-                                             int n_top = 0) {
+                                             uint32_t guard_lim = kGuardTrips) {
     const bool any = MODE == 0 ? any_lane : MODE == 2;
     const V3 inv = ray_inv(d);
     V3 oi = o * inv;
     // near plane index per axis (0 = lo, 1 = hi) from the sign of 1/d
-    const int sx = __float_as_int(inv.x) < 0 ? 1 : 0, sy = __float_as_int(inv.y) < 0 ? 1 : 0,
-              sz = __float_as_int(inv.z) < 0 ? 1 : 0;
+    int sx = __float_as_int(inv.x) < 0 ? 1 : 0, sy = __float_as_int(inv.y) < 0 ? 1 : 0,
+        sz = __float_as_int(inv.z) < 0 ? 1 : 0;
+    if (OCT) sx = 7 * (sx | (sy << 1) | (sz << 2));   // octant copy offset (visit_node4)
     TState ts;
     if (RES) ts = *tsp;
     else tstate_init(ts, stk, tmax);
@@ -541,8 +565,8 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     int cur = ts.cur;
     int leaf = ts.leaf;
     do {
-        while (cur >= 0 && cur != kSentinel) {
-            visit_node4<STATS, MODE, S, QN, TOP>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn, top, n_top);
+        while (cur >= 0 && cur != S::kSent) {
+            visit_node4<STATS, MODE, S, QN, OCT>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn);
             if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
@@ -572,7 +596,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 if (mt_u(xyz(q0), xyz(q1), xyz(q2), o, d, tmin, best, id, best_id, any, t)) {
                     best = t;
                     best_id = id;
-                    if (any) { cur = kSentinel; break; }
+                    if (any) { cur = S::kSent; break; }
                 }
             }
             if (any && best_id >= 0) { leaf = 0; break; }
@@ -585,20 +609,20 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
             // (they keep it postponed); 0: drain every lane's chain of leaves first
             if (__popcll(__ballot(leaf < 0)) <= (uint32_t)leaf_exit) break;
         }
-        if (RES && (cur != kSentinel || leaf < 0) && __popcll(__ballot(true)) < min_lanes) break;
+        if (RES && (cur != S::kSent || leaf < 0) && __popcll(__ballot(true)) < min_lanes) break;
         // watchdog: a traversal revisiting nodes forever (corrupt tree) ends the query and
         // raises the fault flag that the host turns into an error, instead of hanging the GPU
         if (++guard > guard_lim) {
             if (fault) atomicOr(fault, 1);
-            cur = kSentinel;
+            cur = S::kSent;
             leaf = 0;
         }
-    } while (cur != kSentinel || leaf < 0);
+    } while (cur != S::kSent || leaf < 0);
     hit_id = best_id;
     hit_t = best;
     if (RES) {
         tsp->cur = cur; tsp->leaf = leaf; tsp->sp = sp; tsp->best_id = best_id; tsp->best = best;
-        return !(cur != kSentinel || leaf < 0);
+        return !(cur != S::kSent || leaf < 0);
     }
     return best_id >= 0;
 }
@@ -700,13 +724,18 @@ void trace_kernel(TraceParams P) {
     constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
     constexpr bool MIS = (VAR & 256) != 0;     // MIS direct lighting (sample_direct_lighting2) instead of NEE
     constexpr bool FSQ = SCENE_LDS;            // shading sqrt fast path (sqrt_cr)
-    constexpr bool TOPN = (VAR & 512) != 0;    // quantised nodes [0, n_top) in LDS
     extern __shared__ float4 smem[];
-    constexpr int kStackWords = STACK;
-    int* lstack = reinterpret_cast<int*>(smem) + threadIdx.x;
-    using StackT = typename std::conditional<SPILL, SpillStack<STACK>, LdsStack>::type;
+    // LDS: the traversal stacks (16-bit entries for LDS-resident scenes), then the scene copy
+    using StackT = typename std::conditional<SPILL, SpillStack<STACK>,
+                                             typename std::conditional<SCENE_LDS, LdsStack16, LdsStack>::type>::type;
+    constexpr int kStackF4 = STACK * kBlock * (SCENE_LDS ? 2 : 4) / 16;
     StackT stk;
-    stk.l = lstack;
+    if constexpr (SCENE_LDS) {
+        const int t = threadIdx.x;
+        stk.l = reinterpret_cast<short*>(smem) + (t & ~63) + 2 * (t & 31) + ((t >> 5) & 1);
+    } else {
+        stk.l = reinterpret_cast<int*>(smem) + threadIdx.x;
+    }
     if constexpr (SPILL) {
         stk.g = P.spill + (size_t)blockIdx.x * kBlock + threadIdx.x;
         stk.gs = gridDim.x * kBlock;
@@ -721,14 +750,28 @@ void trace_kernel(TraceParams P) {
     if (SCENE_LDS) {
         // small scene: copy BVH + triangles, and the shading data (normals, frames,
         // materials, emitters), into LDS once per persistent block
-        float4* sn = smem + kStackWords * kBlock / 4;
-        float4* st4 = sn + P.n_node_f4;
+        float4* sn = smem + kStackF4;
+        const int n_node4 = P.n_node_f4 / 8;
+        float4* st4 = sn + 56 * n_node4;
         float4* snm = st4 + P.n_tri_f4;
         float4* sfr = snm + P.n_tri;
         float4* smt = sfr + 6 * P.n_tri;
         float4* slv = smt + 2 * P.n_mat;
         int* slo = reinterpret_cast<int*>(slv + 4 * P.n_lt);
-        for (int i = threadIdx.x; i < P.n_node_f4; i += kBlock) sn[i] = P.nodes[i];
+        // octant copies of the BVH4 (visit_node4 OCT): copy k of node n holds the near / far
+        // planes of each axis for the direction signs k = sx | sy << 1 | sz << 2, then the refs
+        // with the empty-slot reference rewritten to the 16-bit stack's sentinel
+        for (int i = threadIdx.x; i < 56 * n_node4; i += kBlock) {
+            const int n = i / 56, r = i - 56 * n, k = r / 7, slot = r - 7 * k;
+            const int ax = slot >> 1, sgn = (k >> ax) & 1, far = slot & 1;
+            const float4* src = P.nodes + 8 * n;
+            float4 v = slot == 6 ? src[6] : src[2 * ax + (sgn ^ far)];
+            if (slot == 6) {
+                int* rr = reinterpret_cast<int*>(&v);
+                for (int c = 0; c < 4; ++c) rr[c] = rr[c] == kSentinel ? LdsStack16::kSent : rr[c];
+            }
+            sn[i] = v;
+        }
         for (int i = threadIdx.x; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
         for (int i = threadIdx.x; i < P.n_tri; i += kBlock) snm[i] = P.tri_nm[i];
         for (int i = threadIdx.x; i < 6 * P.n_tri; i += kBlock) sfr[i] = P.tri_frame[i];
@@ -743,17 +786,6 @@ void trace_kernel(TraceParams P) {
         s_mats = reinterpret_cast<const float*>(smt);
         s_lv = slv;
         s_loff = slo;
-    }
-    const float4* g_top = nullptr;
-    int n_top = 0;
-    if constexpr (TOPN) {
-        // the breadth-first top of the tree (collapse_bvh4 numbers it first), once per block
-        float4* st4 = smem + kStackWords * kBlock / 4;
-        for (int i = threadIdx.x; i < 4 * P.n_top; i += kBlock) st4[i] = P.nodes[i];
-        __syncthreads();
-        g_top = st4;
-        n_top = P.n_top;
-        asm volatile("" : "+s"(n_top));
     }
     const int lane = threadIdx.x & 63;
     // diagnostic (P.wave_clock, env PRT_WAVE_CLOCK): each wave's start / end real time and the
@@ -906,28 +938,28 @@ void trace_kernel(TraceParams P) {
             const int res_min = exhausted ? 0 : P.resume_min;
             bool done;
             if (PHASE && do_shadow)
-                done = traverse_ww4<STATS, 2, StackT, QNODE, true, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
-                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim, g_top, n_top);
+                done = traverse_ww4<STATS, 2, StackT, QNODE, true, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
             else if (PHASE)
-                done = traverse_ww4<STATS, 1, StackT, QNODE, true, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
-                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim, g_top, n_top);
+                done = traverse_ww4<STATS, 1, StackT, QNODE, true, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
             else
-                done = traverse_ww4<STATS, 0, StackT, QNODE, true, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax,
+                done = traverse_ww4<STATS, 0, StackT, QNODE, true, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax,
                                                                   qtype == Q_SHADOW, stk, hid, ht, cn, &tst, res_min,
-                                                                  P.fault, lb, le, glim, g_top, n_top);
+                                                                  P.fault, lb, le, glim);
             pending = !done;
             if (pending) continue;   // resume next iteration; no shading yet
             hit = hid >= 0;
         } else if (PHASE) {
             if (do_shadow)
-                hit = traverse_ww4<STATS, 2, StackT, QNODE, false, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
-                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim, g_top, n_top);
+                hit = traverse_ww4<STATS, 2, StackT, QNODE, false, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
+                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
             else
-                hit = traverse_ww4<STATS, 1, StackT, QNODE, false, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
-                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim, g_top, n_top);
+                hit = traverse_ww4<STATS, 1, StackT, QNODE, false, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
+                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
         } else {
-            hit = traverse_ww4<STATS, 0, StackT, QNODE, false, TOPN>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
-                                                              stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim, g_top, n_top);
+            hit = traverse_ww4<STATS, 0, StackT, QNODE, false, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
+                                                              stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim);
         }
 
         if (STATS) {
@@ -1248,8 +1280,7 @@ void trace_kernel(TraceParams P) {
     X(kVarLdsAnyOcc, 8, true, 1)              \
     X(kVarGlobal, 224, false, 6)              \
     X(kVarLdsMis, 256, true, 6)               \
-    X(kVarGlobalMis, 480, false, 6)           \
-    X(kVarGlobalTop, 736, false, 6)
+    X(kVarGlobalMis, 480, false, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>

@@ -49,9 +49,6 @@ struct Bvh4Host {
     int32_t depth = 0;             // max root-to-leaf node count - 1
     int32_t stack_need = 0;        // worst-case traversal stack entries (3 per level + sentinel)
 };
-// The first min(kTopNodesMax, n) nodes of the collapsed BVH4 are its breadth-first top;
-// the global-scene kernel keeps up to that many (quantised) in LDS.
-constexpr int64_t kTopNodesMax = 256;
 void collapse_bvh4(const BvhHost& b2, Bvh4Host* out);
 
 // Quantised BVH4 for scenes read from HBM: one node = 4 x float4 = 64 B (two per

@@ -48,7 +48,6 @@ struct TraceParams {
     const float4* sph;        // center xyz, radius
     const int* sph_mat;
     unsigned long long* wave_clock;  // diagnostic: per wave (start, end, items) real-time stamps, or null
-    int n_top;                // top-level variants: leading (breadth-first) quantised nodes copied to LDS
 };
 
 // trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the
@@ -61,14 +60,12 @@ constexpr int kVarGlobal = 3;      // global scene: quantised 64-B nodes, LDS st
 // estimator variants: the reference's unused MIS direct lighting (PRT_FLAG_MIS_NEE)
 constexpr int kVarLdsMis = 4;      // LDS scene, mixed schedule, >= 6 waves/SIMD
 constexpr int kVarGlobalMis = 5;   // kVarGlobal + MIS
-constexpr int kVarGlobalTop = 6;   // kVarGlobal + the breadth-first top of the tree in LDS (n_top nodes)
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 6;
+constexpr int kVarLast = 5;
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
 bool variant_quantized(int var);
-bool variant_top(int var);
 
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);

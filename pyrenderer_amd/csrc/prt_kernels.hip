@@ -125,15 +125,17 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
 // entries needed: one per level (<= depth) plus the while-while sentinel
 int stack_variant(int depth) { return depth + 1 <= 10 ? 10 : depth + 1 <= 16 ? 16 : depth + 1 <= 32 ? 32 : 64; }
 
+// LDS-resident scene (prt_device.h trace_kernel): the BVH4 as 8 octant copies of 7 float4 per
+// node (n_node_f4 counts the 8 float4 of a global BVH4 node), triangles, shading data
 size_t lds_scene_bytes(const TraceParams& P) {
-    return 16 * ((size_t)P.n_node_f4 + P.n_tri_f4 + 7 * (size_t)P.n_tri + 2 * (size_t)P.n_mat + 4 * (size_t)P.n_lt) +
+    return 16 * (7 * (size_t)P.n_node_f4 + P.n_tri_f4 + 7 * (size_t)P.n_tri + 2 * (size_t)P.n_mat + 4 * (size_t)P.n_lt) +
            4 * ((size_t)P.n_light + 1);
 }
 
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
-    size_t b = (size_t)stack * kBlock * sizeof(int);
+    // traversal stack entries: 16-bit for LDS-resident scenes, 32-bit otherwise
+    size_t b = (size_t)stack * kBlock * (variant_uses_lds(var) ? sizeof(short) : sizeof(int));
     if (variant_uses_lds(var)) b += lds_scene_bytes(P);
-    if (variant_top(var)) b += 64 * (size_t)P.n_top;
     return b;
 }
 
@@ -195,15 +197,6 @@ bool variant_mis(int var) {
 bool variant_quantized(int var) {
     switch (var) {
 #define X(id, bits, lds, wpe) case id: return (bits & 64) != 0;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
-
-bool variant_top(int var) {
-    switch (var) {
-#define X(id, bits, lds, wpe) case id: return (bits & 512) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;
