@@ -304,7 +304,8 @@ __device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, 
     float t = -f * dot(q, e1);
     float u = -f * dot(q, d);
     float v = f * dot(c, s);
-    const bool in_range = t0 < t && (t < tbest || (!any && t == tbest && id < best_id));
+    // bitwise (not short-circuit) combination: one lane mask, no exec-mask branches
+    const bool in_range = (t0 < t) & ((t < tbest) | ((!any) & (t == tbest) & (id < best_id)));
     const bool hit = nz & in_range & (0.0f <= u) & (u <= 1.0f) & (v >= 0.0f) & (1.0f - u - v >= 0.0f);
     tout = t;
     return hit;
@@ -517,23 +518,24 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
             sp -= h3 ? 0 : 1;
         } else {
             // nearest hit child first by a 3-comparator tournament on the entry distances
-            // (misses count as +inf); the three others are pushed when hit: the loser of each
-            // pair is a hit iff both of the pair are, the loser of the final iff each pair
-            // has a hit
+            // (misses count as +inf, a hit's distance is finite); the three others are pushed
+            // when hit, i.e. when their key is finite: the loser of each pair, then the loser
+            // of the final.  Keys and masks stay floats / lane masks (no 0/1 integers).
             const float k0 = h0 ? t0 : INFINITY, k1 = h1 ? t1 : INFINITY;
             const float k2 = h2 ? t2 : INFINITY, k3 = h3 ? t3 : INFINITY;
             const bool m01 = k1 < k0, m23 = k3 < k2;
-            const float a = m01 ? k1 : k0, c = m23 ? k3 : k2;
+            const float a = m01 ? k1 : k0, xb = m01 ? k0 : k1;
+            const float c = m23 ? k3 : k2, xd = m23 ? k2 : k3;
             const int ra = m01 ? r1 : r0, rb = m01 ? r0 : r1;
             const int rc = m23 ? r3 : r2, rd = m23 ? r2 : r3;
             const bool m = c < a;
             const int rn = m ? rc : ra, rl = m ? ra : rc;
-            const bool p01 = h0 | h1, p23 = h2 | h3;
-            st.put(sp + 1, rb); sp += (h0 & h1) ? 1 : 0;
-            st.put(sp + 1, rd); sp += (h2 & h3) ? 1 : 0;
-            st.put(sp + 1, rl); sp += (p01 & p23) ? 1 : 0;
+            const float xn = m ? c : a, xl = m ? a : c;
+            st.put(sp + 1, rb); sp += xb < INFINITY ? 1 : 0;
+            st.put(sp + 1, rd); sp += xd < INFINITY ? 1 : 0;
+            st.put(sp + 1, rl); sp += xl < INFINITY ? 1 : 0;
             const int tp = st.get(sp);
-            const bool any_hit = p01 | p23;
+            const bool any_hit = xn < INFINITY;
             cur = any_hit ? rn : tp;
             sp -= any_hit ? 0 : 1;
         }
