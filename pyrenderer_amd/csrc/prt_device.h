@@ -298,7 +298,7 @@ __device__ __forceinline__ bool mt_u(V3 v0, V3 e1, V3 e2, V3 o, V3 d, float t0, 
     V3 c = cross(e1, d);
     float det = dot(c, e2);
     const bool nz = fabsf(det) > 0.0f;
-    float f = rcp_exact(nz ? det : 1.0f);
+    float f = rcp_exact(det);   // det == 0 takes rcp_exact's division (inf): masked by nz below
     V3 s = o - v0;
     V3 q = cross(s, e2);
     float t = -f * dot(q, e1);
