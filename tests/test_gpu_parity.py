@@ -135,6 +135,29 @@ def test_triangle_soup_matches_oracle(cornell):
     assert same >= 0.999, same
 
 
+def test_lds_soup_deep_stack_matches_oracle(cornell):
+    """A scene still LDS-resident but with a deeper BVH4 than the Cornell box: the octant
+    node copies and the 16-bit traversal stack (16 entries) of the LDS kernels, against the
+    oracle and against the global-scene kernel on the same scene."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    flat = _soup_scene(cornell, 12, 11)
+    ds = DeviceScene(flat, 0)
+    k = ds.kernel_info()
+    assert k["lds_scene"] and k["stack"] >= 16 and ds.bvh_depth > 4, (k, ds.bvh_depth)
+    osc = O.OracleScene.from_flat(flat)
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    g = _gpu_frame(ds, cam, 64, 64, 4, 8, seed=4)
+    o = osc.render(cam, 64, 64, 4, 8, seed=4)
+    np.testing.assert_array_equal(g, o)
+    from pyrenderer_amd.device_scene import interleaved_tiles
+    ids = interleaved_tiles(64, 64, 32)
+    a, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 4, N.VAR_LDS << 8)
+    b, _ = ds.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 4, N.VAR_GLOBAL << 8)
+    np.testing.assert_array_equal(a, b)
+    ds.close()
+
+
 def test_full_size_config2_matches_oracle(gpu_scene, oracle_scene, cornell):
     """BASELINE config 2 at full size (512^2 x 64 spp, depth 8), the WHOLE frame
     against the oracle (brute-force closest hits, all host threads).  At this size
