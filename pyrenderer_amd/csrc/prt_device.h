@@ -471,7 +471,8 @@ __device__ __forceinline__ V3 ray_inv(V3 d) {
 // an octant copy take the first hit child instead of sorting entry distances (see step).
 template <bool STATS, int MODE, class S, bool QN, bool OCT = false>
 __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, int& cur, int& sp, S stk, V3 inv, V3 oi,
-                                            int sx, int sy, int sz, float tmin, float best, Counters& cn) {
+                                            int sx, int sy, int sz, float tmin, float best, Counters& cn,
+                                            bool any_lane = false) {
     float t0, t1, t2, t3;
     bool h0, h1, h2, h3;
     int r0, r1, r2, r3;
@@ -539,6 +540,11 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
             // (misses count as +inf, a hit's distance is finite); the three others are pushed
             // when hit, i.e. when their key is finite: the loser of each pair, then the loser
             // of the final.  Keys and masks stay floats / lane masks (no 0/1 integers).
+            // any-hit lanes of a mixed wave (MODE 0, global scenes): farthest hit child first —
+            // keys negated (entry distances are >= tmin > 0; misses stay +inf).  A shadow ray ends
+            // at the light, and an occluder near that end ends the query: C4 18.85 -> 18.67 ms
+            // (the LDS scenes' shadow iterations go back to front for the same reason, MODE 2)
+            if (MODE == 0 && any_lane) { t0 = -t0; t1 = -t1; t2 = -t2; t3 = -t3; }
             const float k0 = h0 ? t0 : INFINITY, k1 = h1 ? t1 : INFINITY;
             const float k2 = h2 ? t2 : INFINITY, k3 = h3 ? t3 : INFINITY;
             const bool m01 = k1 < k0, m23 = k3 < k2;
@@ -586,7 +592,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     int leaf = ts.leaf;
     do {
         while (cur >= 0 && cur != S::kSent) {
-            visit_node4<STATS, MODE, S, QN, OCT>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn);
+            visit_node4<STATS, MODE, S, QN, OCT>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn, any);
             if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
