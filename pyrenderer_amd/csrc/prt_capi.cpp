@@ -118,7 +118,7 @@ struct Scene {
     int stack4 = 0;                  // stack variant for the BVH4 (0 = BVH4 unusable)
     int need4 = 0;                   // worst-case BVH4 traversal stack entries
     int leaf_break = -1;             // env PRT_LEAF_BREAK (0..64); -1: per variant (trace launch)
-    int leaf_exit = 8;               // env PRT_LEAF_EXIT (0..64); C2 5.25 -> 5.04 ms, C4 29.8 -> 28.8 ms
+    int leaf_exit = -1;              // env PRT_LEAF_EXIT (0..64); -1: per variant (trace launch)
     int resume_min = 32;             // resume variants (env PRT_RESUME_MIN; C4 after the r02 BVH fixes: 16 / 24 / 32 / 40 / 48 -> 19.4 / 19.1 / 19.0 / 19.4 / 19.8 ms)
     uint32_t guard_trips = 1u << 20; // traversal phases per query before the watchdog trips (env PRT_GUARD_TRIPS)
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
@@ -370,9 +370,13 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
     // while-while leaf-phase entry: LDS scenes wait for every descending lane's leaf (their
     // leaves are cheap and traversals short); global scenes enter the leaf phase once at
-    // most 8 descending lanes still lack one (C4: 35.1 -> 29.7 ms; C2 prefers 0)
-    P.leaf_break = s->leaf_break >= 0 ? s->leaf_break : (prt::variant_uses_lds(var) ? 0 : 8);
-    P.leaf_exit = s->leaf_exit;
+    // most 16 descending lanes still lack one (C4: 35.1 -> 29.7 ms at 8 in round 1, 18.69 ->
+    // 18.44 ms at 16 with leaf exit 12 after the round-2 traversal changes; C2 prefers 0).
+    // Leaf-phase exit: back to descending once at most 8 (LDS) / 12 (global) lanes still
+    // hold a leaf (C2 5.25 -> 5.04 ms in round 1, flat for 8-16 now)
+    const bool lds_var = prt::variant_uses_lds(var);
+    P.leaf_break = s->leaf_break >= 0 ? s->leaf_break : (lds_var ? 0 : 16);
+    P.leaf_exit = s->leaf_exit >= 0 ? s->leaf_exit : (lds_var ? 8 : 12);
     int& occ = s->occ[2 * var + (stats ? 1 : 0)];
     if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(stack, var, stats, prt::trace_smem_bytes(stack, var, P)));
     if (spill) {
