@@ -50,9 +50,10 @@ extern "C" {
  * Selects the MIS kernel variants (4, 5); an explicit variant must agree with the flag. */
 #define PRT_FLAG_MIS_NEE 0x8u
 /* trace-kernel variant in bits 8..15 (0 = automatic; the numbering is the
- * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: 1 LDS-resident scene, 2 the same
- * without an occupancy target, 3 global scene (quantised nodes, spill stack), 4 / 5 the
- * MIS estimator on an LDS / global scene).  Variants of one estimator produce
+ * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: 1 LDS-resident scene (>= 7 waves per
+ * SIMD), 2 the same without an occupancy target, 3 global scene (quantised nodes, spill
+ * stack), 4 / 5 the MIS estimator on an LDS / global scene, 6 the LDS-resident scene built
+ * for >= 6 waves per SIMD).  Variants of one estimator produce
  * bit-identical images; the selector exists for A/B runs and tests. */
 #define PRT_FLAG_VARIANT_SHIFT 8
 #define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFFu) << PRT_FLAG_VARIANT_SHIFT)

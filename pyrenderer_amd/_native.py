@@ -18,12 +18,13 @@ PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
 PRT_FLAG_MIS_NEE = 0x8
 # trace-kernel variant ids 1..VAR_LAST of the reference estimator (pyrenderer_amd/csrc/prt_kernels.h
 # kVar*); the MIS direct-lighting estimator's variants (PRT_FLAG_MIS_NEE) follow
-VAR_LDS = 1           # LDS-resident scene, phase-aligned schedule, >= 6 waves/SIMD
+VAR_LDS = 1           # LDS-resident scene, phase-aligned schedule, >= 7 waves/SIMD
 VAR_LDS_ANY_OCC = 2   # ... without the occupancy target
 VAR_GLOBAL = 3        # scene in HBM: quantised BVH4, LDS stack + global spill, suspended tails
 VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL)
-VAR_LAST = 5
+VAR_LDS6 = 6          # VAR_LDS built for >= 6 waves/SIMD (LDS copies that fit 6 but not 7 blocks per CU)
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6)
+VAR_LAST = 6
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 

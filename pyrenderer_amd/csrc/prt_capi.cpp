@@ -247,8 +247,8 @@ bool lds_fits4(const Scene* s) {
     const int64_t n_refs = s->n_tri_f4 / 3;
     return (int64_t)prt::lds_scene_bytes(P) <= kLdsSceneBytes && s->n_node4_f4 / 8 < 0x7FFF && n_refs * 8 <= 32768;
 }
-// LDS-resident scene when it fits; the >= 6 waves/SIMD build when six blocks' LDS
-// still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
+// LDS-resident scene when it fits; the >= 7 (>= 6) waves/SIMD build when seven (six) blocks'
+// LDS still fit one CU (160 KiB), so the occupancy target is not defeated by LDS.
 // Everything else (and BVH4s deeper than the 64-entry LDS stack) takes the global-scene
 // kernel: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal tails,
 // >= 6 waves/SIMD (C4: 28.6 ms at 5 waves, 27.2 at 6, 28.6 at 7 with spills).
@@ -258,7 +258,7 @@ int default_variant(const Scene* s) {
     std::memset(&P, 0, sizeof(P));
     scene_sizes(s, P);
     size_t smem = prt::trace_smem_bytes(s->stack4, prt::kVarLds, P);
-    return smem * 6 <= 160 * 1024 ? prt::kVarLds : prt::kVarLdsAnyOcc;
+    return smem * 7 <= 160 * 1024 ? prt::kVarLds : smem * 6 <= 160 * 1024 ? prt::kVarLds6 : prt::kVarLdsAnyOcc;
 }
 // the traversal stack entries of variant `var` (LDS part for the spill variants)
 int variant_stack(const Scene* s, int var) { return prt::variant_spills(var) ? s->spill_lds : s->stack4; }

@@ -1325,10 +1325,11 @@ void trace_kernel(TraceParams P) {
 
 // variant table: (VAR bits of trace_kernel, LDS-resident scene, min waves per SIMD); see prt_kernels.h
 #define PRT_VARIANTS(X)                       \
-    X(kVarLds, 8, true, 6)                    \
+    X(kVarLds, 8, true, 7)                    \
     X(kVarLdsAnyOcc, 8, true, 1)              \
     X(kVarGlobal, 224, false, 6)              \
     X(kVarLdsMis, 256, true, 6)               \
+    X(kVarLds6, 8, true, 6)                   \
     X(kVarGlobalMis, 480, false, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64

@@ -53,15 +53,18 @@ struct TraceParams {
 // trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the
 // while-while BVH4 traversal (prt_device.h traverse_ww4) and give bit-identical images;
 // the measured history of the variants this set replaced is in DESIGN.md §2.
-constexpr int kVarLds = 1;         // LDS-resident scene, phase-aligned ext/shadow iterations, >= 6 waves/SIMD
+constexpr int kVarLds = 1;         // LDS-resident scene, phase-aligned ext/shadow iterations, >= 7 waves/SIMD
+                                   // (72 VGPRs: C2 4.40 -> 4.23 ms against the 6-wave build)
 constexpr int kVarLdsAnyOcc = 2;   // ... no occupancy target (LDS scenes too large for 6 blocks per CU)
 constexpr int kVarGlobal = 3;      // global scene: quantised 64-B nodes, LDS stack + global spill area,
                                    // suspended traversal tails, >= 6 waves/SIMD
 // estimator variants: the reference's unused MIS direct lighting (PRT_FLAG_MIS_NEE)
 constexpr int kVarLdsMis = 4;      // LDS scene, mixed schedule, >= 6 waves/SIMD
 constexpr int kVarGlobalMis = 5;   // kVarGlobal + MIS
+constexpr int kVarLds6 = 6;        // kVarLds built for >= 6 waves/SIMD (80 VGPRs): LDS scenes whose copy
+                                   // fits six blocks per CU but not seven
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 5;
+constexpr int kVarLast = 6;
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
