@@ -477,7 +477,9 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     bool h0, h1, h2, h3;
     int r0, r1, r2, r3;
     if (QN) {
-        const float4* nd = nodes + (size_t)cur * 4;
+        // 64-B nodes at a 32-bit byte offset from the uniform base (saddr + voffset addressing,
+        // no 64-bit address arithmetic): BVH4 nodes < refs / 3 < 2^25, so the offset < 2^31
+        const float4* nd = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + ((uint32_t)cur << 6));
         float4 a = nd[0], b = nd[1], c = nd[2], rf = nd[3];
         if (STATS) { cn.nodes++; cn.it_inner++; }
         QAxis X = {a.w * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
@@ -807,10 +809,12 @@ void trace_kernel(TraceParams P) {
                 const float nxv[4] = {lx.x, lx.y, lx.z, lx.w}, fxv[4] = {hx.x, hx.y, hx.z, hx.w};
                 const float nyv[4] = {ly.x, ly.y, ly.z, ly.w}, fyv[4] = {hy.x, hy.y, hy.z, hy.w};
                 const float nzv[4] = {lz.x, lz.y, lz.z, lz.w}, fzv[4] = {hz.x, hz.y, hz.z, hz.w};
-                for (int c = 0; c < 4; ++c)
+                for (int c = 0; c < 4; ++c) {
                     key[c] = rr[c] == kSentinel ? INFINITY
                                                 : ((k & 1) ? -fxv[c] : nxv[c]) + ((k & 2) ? -fyv[c] : nyv[c]) +
                                                       ((k & 4) ? -fzv[c] : nzv[c]);
+                    if (!(key[c] == key[c])) key[c] = INFINITY;   // NaN (degenerate box): a total order
+                }
             }
             const float vin[4] = {v.x, v.y, v.z, v.w};
             float vout[4];

@@ -1,0 +1,30 @@
+#!/bin/bash
+# After tools/s4_full.sh <dir> ran on the GPU box: merge its PMC passes into profiles/pmc.json
+# and copy the rocprof summaries, counter CSVs, bench lines and test log into profiles/<dest>.
+#   bash tools/s4_collect.sh gpurun_out/s4e profiles/r02/s4
+set -e
+SRC=$1; DST=$2
+python tools/pmc_summary.py --dir $SRC/prof_c2 --key cornell_512x512x64spp_d8 > /dev/null
+python tools/pmc_summary.py --dir $SRC/prof_c4 --key cubes_512x512x64spp_d8 > /dev/null
+for c in prof_c2 prof_c4; do
+  rm -rf $DST/$c; mkdir -p $DST/$c/fetch $DST/$c/write $DST/$c/sq
+  cp $SRC/$c/bench.json $SRC/$c/bench_under_rocprof.json $DST/$c/
+  cp $SRC/$c/trace/k_kernel_stats.csv $DST/$c/kernel_stats.csv
+  for p in fetch write sq; do cp $SRC/$c/$p/*counter_collection.csv $DST/$c/$p/; done
+done
+mkdir -p $DST/bench_all && cp $SRC/bench_all/c*.json $DST/bench_all/ && cp $SRC/pytest_gpu.log $DST/
+python - "$SRC" <<'PY'
+import json, sys
+src = sys.argv[1]
+for c in range(1, 6):
+    d = json.loads(open(f'{src}/bench_all/c{c}.json').read().strip().splitlines()[-1]); r = d['roofline']
+    print(c, d['value'], d['ms_per_step'], r['bound'], r.get('frac'), r.get('kernel_avg_ms'), (d['cpu_baseline'] or {}).get('value'))
+d = json.load(open('profiles/pmc.json'))
+for k, v in d.items():
+    print(k, v['kernel_sha'], v['valu_issue_util'], v['valu_lane_util'], round(v['hbm_bytes_per_launch'] / 1e9, 3),
+          round(v['hbm_bytes_raw'] / 1e9, 3), v['dispatch_ms'])
+for c in (2, 4):
+    d = json.loads(open(f'{src}/prof_c{c}/bench.json').read().strip().splitlines()[-1])
+    print('prof', c, d['value'], d['roofline']['kernel_avg_ms'])
+    print(open(f'{src}/prof_c{c}/trace/k_kernel_stats.csv').read().splitlines()[1][:130])
+PY
