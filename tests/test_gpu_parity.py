@@ -121,6 +121,42 @@ def _soup_scene(cornell, n_extra, seed):
     return FlatScene(tri_v, tri_n, tri_mat, tri_prim, lo, hi, f.mat, f.light_tri + n_extra, f.light_off, f.direct_rgb)
 
 
+@pytest.mark.parametrize("n_extra", [0, 6, 12, 20, 40])
+def test_default_variant_reaches_its_occupancy(cornell, n_extra):
+    """The default kernel is chosen by how many blocks' LDS fit one CU: the >= 7-waves LDS build
+    (variant 1) must actually get 7 blocks per CU, the >= 6-waves one (variant 6) 6, the global
+    scene kernel (3) 6 — otherwise an occupancy target would be paid for in registers and not
+    collected; an LDS copy too large for six blocks takes the untargeted build (2, <= 5 blocks).
+    Each scene also renders bit-identically to the oracle with that variant."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    flat = _soup_scene(cornell, n_extra, 11) if n_extra else cornell[2]
+    ds = DeviceScene(flat, 0)
+    var = ds.kernel_info()["variant"]
+    want = {N.VAR_LDS: (7,), N.VAR_LDS6: (6,), N.VAR_GLOBAL: (6,), N.VAR_LDS_ANY_OCC: (1, 2, 3, 4, 5)}
+    assert var in want, var
+    assert ds.blocks_per_cu in want[var], (n_extra, var, ds.blocks_per_cu)
+    osc = O.OracleScene.from_flat(flat)
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    g = _gpu_frame(ds, cam, 32, 32, 2, 6, seed=5)
+    o = osc.render(cam, 32, 32, 2, 6, seed=5)
+    np.testing.assert_array_equal(g, o)
+    ds.close()
+
+
+def test_default_variants_cover_both_lds_builds(cornell):
+    """Among the scenes above, both LDS builds are defaults somewhere (the 6-wave build is not
+    dead code)."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    seen = set()
+    for n_extra in (0, 6, 12, 20):
+        ds = DeviceScene(_soup_scene(cornell, n_extra, 11) if n_extra else cornell[2], 0)
+        seen.add(ds.kernel_info()["variant"])
+        ds.close()
+    assert {N.VAR_LDS, N.VAR_LDS6} <= seen, seen
+
+
 def test_triangle_soup_matches_oracle(cornell):
     from pyrenderer_amd.device_scene import DeviceScene
     flat = _soup_scene(cornell, 3000, 9)
