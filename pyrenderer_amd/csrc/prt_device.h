@@ -817,12 +817,18 @@ void trace_kernel(TraceParams P) {
                 }
             }
             const float vin[4] = {v.x, v.y, v.z, v.w};
-            float vout[4];
+            int rank[4];   // position of child c in the order (a permutation of 0..3)
+#pragma unroll
             for (int c = 0; c < 4; ++c) {
-                int rank = 0;   // position of child c in the order
-                for (int e = 0; e < 4; ++e) rank += (key[e] < key[c] || (key[e] == key[c] && e < c)) ? 1 : 0;
-                vout[rank] = vin[c];
+                rank[c] = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rank[c] += (key[e] < key[c] || (key[e] == key[c] && e < c)) ? 1 : 0;
             }
+            // slot j takes the child of rank j (selects, no dynamically indexed array in scratch)
+            float vout[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                vout[j] = rank[0] == j ? vin[0] : rank[1] == j ? vin[1] : rank[2] == j ? vin[2] : vin[3];
             sn[i] = make_float4(vout[0], vout[1], vout[2], vout[3]);
         }
         for (int i = threadIdx.x; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
