@@ -68,6 +68,9 @@ def build(force=False, verbose=False, out=None, defs=()):
     os.makedirs(os.path.dirname(os.path.abspath(lib)), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     extra = [f"-D{d}" for d in defs]
+    if out is not None:
+        # A/B builds only: extra compiler flags (e.g. "-mllvm --amdgpu-use-amdgpu-trackers")
+        extra += os.environ.get("PRT_AB_FLAGS", "").split()
     units = [(os.path.join(CSRC, f), os.path.join(obj_dir, os.path.splitext(f)[0] + ".o"), []) for f in SOURCES]
     units += [(os.path.join(CSRC, TRACE_INST), os.path.join(obj_dir, f"prt_trace_{st}_{tt}.o"),
                [f"-DPRT_STACK={st}", f"-DPRT_STATS={tt}"]) for st, tt in TRACE_SETS]
