@@ -312,7 +312,8 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     const bool stats = (flags & PRT_FLAG_STATS) != 0;
     const bool timed = (flags & PRT_FLAG_TIME) != 0;
     if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), stream));
-    HIP_TRY(hipMemsetAsync((char*)cx->work.p + kFaultOffset, 0, sizeof(int), stream));
+    // the watchdog flag is cleared once per render: by the first chunk's camera kernel, else here
+    if (!primary) HIP_TRY(hipMemsetAsync((char*)cx->work.p + kFaultOffset, 0, sizeof(int), stream));
 
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
@@ -403,8 +404,15 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         P.n_items = (uint64_t)(n * n_slots);
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
-        HIP_TRY(hipMemsetAsync(cx->work.p, 0, 16, stream));
-        if (primary) HIP_TRY(prt::launch_camera(P, (float4*)cx->rays.p, stream));
+        if (primary) {
+            // the camera kernel also zeroes the work counter (and, for the first chunk, the
+            // watchdog flag) ahead of the trace launch: two fewer stream operations per frame
+            P.cam_clears = 1 | (s0 == 0 ? 2 : 0);
+            HIP_TRY(prt::launch_camera(P, (float4*)cx->rays.p, stream));
+            P.cam_clears = 0;
+        } else {
+            HIP_TRY(hipMemsetAsync(cx->work.p, 0, 16, stream));
+        }
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
         DevBuf wclk;
         if (!s->wave_clock_path.empty()) {

@@ -48,6 +48,10 @@ struct TraceParams {
     const float4* sph;        // center xyz, radius
     const int* sph_mat;
     unsigned long long* wave_clock;  // diagnostic: per wave (start, end, items) real-time stamps, or null
+    // camera_kernel clears, before the trace launch that follows it on the stream: bit 0 the work
+    // counter (16 B at `work`), bit 1 the watchdog flag (first chunk of a render only) — instead of
+    // two memset launches per frame
+    int cam_clears;
 };
 
 // trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the

@@ -37,8 +37,16 @@ namespace {
 // (TraceParams::cam_fast), whose origin is the uniform cam_o.
 __global__ __launch_bounds__(kBlock) void camera_kernel(TraceParams P, float4* __restrict__ rays) {
     uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (P.cam_clears & 1) { P.work[0] = 0u; P.work[1] = 0u; P.work[2] = 0u; P.work[3] = 0u; }
+        if (P.cam_clears & 2) *P.fault = 0;
+    }
     if (item >= P.n_items) return;
-    uint32_t cs = (uint32_t)(item / (uint64_t)P.n_slots);
+    // n_slots is a multiple of 64 (tiles of >= 64 px), so the 64 items of a wave share one sample
+    // index: one scalar division per wave from the wave's first item (SGPR operands), instead of
+    // a 64-bit division emulated per lane in VALU
+    const uint64_t item0 = (uint64_t)blockIdx.x * kBlock + (uint32_t)(__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u);
+    const uint32_t cs = (uint32_t)(item0 / (uint64_t)P.n_slots);
     uint32_t slot = (uint32_t)item - cs * (uint32_t)P.n_slots;
     uint32_t xy0 = P.tile_xy[slot >> P.log_tpx];
     int x, y;
