@@ -55,7 +55,12 @@ __global__ __launch_bounds__(kBlock) void camera_kernel(TraceParams P, float4* _
     uint32_t st;
     V3 o, d;
     camera_ray(P, x, y, cs, st, o, d);
-    rays[item] = make_float4(d.x, d.y, d.z, __uint_as_float(st));
+    // the primary rays are read once, by the trace kernel: a nontemporal store keeps them from
+    // displacing the scene in L2 (C2 +0.2 % per bench step; nontemporal accesses inside the trace
+    // kernel were +0.1 % at C2 and -0.3 % at C4, so it keeps plain ones)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v r4 = {d.x, d.y, d.z, __uint_as_float(st)};
+    __builtin_nontemporal_store(r4, reinterpret_cast<f4v*>(rays + item));
 }
 
 // World.hit_all for a batch of rays (intersection_taichi.py:238-291): closest (or any)
@@ -123,7 +128,9 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
     if (!first) { r = acc[3 * (size_t)slot]; g = acc[3 * (size_t)slot + 1]; b = acc[3 * (size_t)slot + 2]; }
     for (int s = 0; s < n_spp; ++s) {
         const float* p = buf + ((size_t)s * n_slots + slot) * 3;
-        r = r + p[0]; g = g + p[1]; b = b + p[2];
+        // per-sample radiance is read once here: nontemporal loads
+        r = r + __builtin_nontemporal_load(p); g = g + __builtin_nontemporal_load(p + 1);
+        b = b + __builtin_nontemporal_load(p + 2);
     }
     acc[3 * (size_t)slot] = r; acc[3 * (size_t)slot + 1] = g; acc[3 * (size_t)slot + 2] = b;
 }
