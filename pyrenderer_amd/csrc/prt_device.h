@@ -876,6 +876,9 @@ void trace_kernel(TraceParams P) {
 
     // diagnostic (STATS) wave-level clocks: refill / traversal / shading, iterations, active lanes
     uint64_t c_refill = 0, c_trav = 0, c_shade = 0, n_iter = 0, n_active = 0;
+    // STATS, phase-aligned schedule: wave clocks and counts of extension / shadow iterations and the
+    // lanes that queried in the shadow ones (diag words 17..21)
+    uint64_t c_it_ext = 0, c_it_sh = 0, n_it_ext = 0, n_it_sh = 0, lanes_sh = 0, t_it = 0;
     uint64_t t_a = 0, t_b = 0;
     // PHASE: the wave alternates extension and shadow iterations, so the costly
     // shading code (run after extension queries only) and the refill execute
@@ -883,7 +886,7 @@ void trace_kernel(TraceParams P) {
     // Lanes whose query kind does not match the wave's phase sit the iteration out.
     bool last_shadow = false;
     while (true) {
-        if (STATS) t_a = __builtin_amdgcn_s_memtime();
+        if (STATS) { t_a = __builtin_amdgcn_s_memtime(); t_it = t_a; }
         bool do_shadow = false;
         if (PHASE) {
             do_shadow = !last_shadow && __ballot(item >= 0 && qtype == Q_SHADOW) != 0;
@@ -981,6 +984,7 @@ void trace_kernel(TraceParams P) {
                 c_refill += t_b - t_a;
                 n_iter++;
                 n_active += (uint64_t)__popcll(active);
+                if (PHASE && do_shadow) lanes_sh += (uint64_t)__popcll(active);
             }
             t_a = t_b;
         }
@@ -1285,7 +1289,12 @@ void trace_kernel(TraceParams P) {
         }
         if (STATS) {
             const bool leader = __builtin_amdgcn_readfirstlane(lane) == lane;
-            if (leader) c_shade += __builtin_amdgcn_s_memtime() - t_a;
+            if (leader) {
+                const uint64_t t_end = __builtin_amdgcn_s_memtime();
+                c_shade += t_end - t_a;
+                if (do_shadow) { c_it_sh += t_end - t_it; n_it_sh++; }
+                else { c_it_ext += t_end - t_it; n_it_ext++; }
+            }
         }
     }
     if (P.wave_clock && lane == 0)
@@ -1305,6 +1314,13 @@ void trace_kernel(TraceParams P) {
             atomicAdd(P.stats + 2, (unsigned long long)c);
             atomicAdd(P.stats + 3, (unsigned long long)e);
             for (int k = 0; k < 7; ++k) atomicAdd(P.stats + 4 + k, (unsigned long long)wv[k]);
+        }
+        {
+            uint64_t ph[5] = {c_it_ext, c_it_sh, n_it_ext, n_it_sh, lanes_sh};
+            for (int k = 0; k < 5; ++k)
+                for (int off = 32; off > 0; off >>= 1) ph[k] += __shfl_down(ph[k], off);
+            if (lane == 0)
+                for (int k = 0; k < 5; ++k) atomicAdd(P.stats + 17 + k, (unsigned long long)ph[k]);
         }
         {
             uint32_t m = cn.max_sp;

@@ -69,7 +69,7 @@ def main():
     from pyrenderer_amd._native import PRT_FLAG_STATS
     for v in a.variants:
         ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, PRT_FLAG_STATS | vflags(v))
-        dg = ds.diag_words().astype(np.float64)
+        dg = ds.diag_words(22).astype(np.float64)   # 17..21: ext / shadow iteration clocks, counts, lanes
         tot = dg[4] + dg[5] + dg[6]
         print(json.dumps({"variant": v, "diag": {"refill_frac": round(dg[4] / tot, 3), "trav_frac": round(dg[5] / tot, 3),
                                                  "shade_frac": round(dg[6] / tot, 3), "wave_iters": int(dg[7]),
@@ -82,7 +82,11 @@ def main():
                                                  "wave_leaf_trips_per_iter": round(dg[10] / max(dg[7], 1), 2),
                                                  "wave_tri_trips_per_iter": round(dg[15] / max(dg[7], 1), 2),
                                                  "max_stack": int(dg[13]),
-                                                 "max_nodes_one_query": int(dg[16])}}),
+                                                 "max_nodes_one_query": int(dg[16]),
+                                                 "shadow_iter_time_frac": round(dg[18] / max(dg[17] + dg[18], 1), 3),
+                                                 "ext_iters": int(dg[19]), "shadow_iters": int(dg[20]),
+                                                 "lanes_per_shadow_iter": round(dg[21] / max(dg[20], 1), 2),
+                                                 "lanes_per_ext_iter": round((dg[8] - dg[21]) / max(dg[19], 1), 2)}}),
               flush=True)
     for v, rows in res.items():
         ms = np.array([x[0] for x in rows])
