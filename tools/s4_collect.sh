@@ -6,7 +6,12 @@ set -e
 SRC=$1; DST=$2
 python tools/pmc_summary.py --dir $SRC/prof_c2 --key cornell_512x512x64spp_d8 > /dev/null
 python tools/pmc_summary.py --dir $SRC/prof_c4 --key cubes_512x512x64spp_d8 > /dev/null
-for c in prof_c2 prof_c4; do
+# configs 1 / 3 / 5 when tools/prof_135.sh ran into the same directory
+[ -d $SRC/prof_c1 ] && python tools/pmc_summary.py --dir $SRC/prof_c1 --key cornell_128x128x4spp_d4 > /dev/null
+[ -d $SRC/prof_c3 ] && python tools/pmc_summary.py --dir $SRC/prof_c3 --key specular_1024x1024x256spp_d8 > /dev/null
+[ -d $SRC/prof_c5 ] && python tools/pmc_summary.py --dir $SRC/prof_c5 --key cornell_4096x4096x256spp_d8 > /dev/null
+for c in prof_c1 prof_c2 prof_c3 prof_c4 prof_c5; do
+  [ -d $SRC/$c ] || continue
   rm -rf $DST/$c; mkdir -p $DST/$c/fetch $DST/$c/write $DST/$c/sq
   cp $SRC/$c/bench.json $SRC/$c/bench_under_rocprof.json $DST/$c/
   cp $SRC/$c/trace/k_kernel_stats.csv $DST/$c/kernel_stats.csv
