@@ -130,7 +130,10 @@ struct Scene {
     uint64_t use_clock = 0;
     std::vector<hipEvent_t> ev;   // start/stop pairs of the last timed call
     int ev_used = 0;
-    size_t chunk_bytes = (size_t)4 << 30;  // per-sample buffer budget (HBM is 288 GB)
+    // per-sample buffer budget of one trace launch (radiance + primary rays): 16 GiB of the 288 GB
+    // of HBM makes config 3 one launch per frame and config 5 eight (4 GiB: 2 and 29), +0.4 / +0.5 %
+    // from the launch tails saved (profiles/r02/s5/chunk_ab/)
+    size_t chunk_bytes = (size_t)16 << 30;
     size_t device_bytes = 0;
     // prt_render / prt_render_multi (as the root): [x][y] output frame, gathered tile sums
     // of every rank and their tile origins (host copy kept alive for the async upload)
@@ -307,6 +310,11 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)s->chunk_bytes / per_sample_all));
     // keep every chunk's item count below 2^31 (32-bit work counter)
     chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, ((int64_t)1 << 31) / n_slots - 1));
+    // equal launches: no short last launch paying a whole launch tail for a few samples
+    {
+        const int64_t nc = (spp + chunk - 1) / chunk;
+        chunk = (spp + nc - 1) / nc;
+    }
     HIP_TRY(cx->buf.ensure((size_t)(chunk * per_sample)));
     if (primary) HIP_TRY(cx->rays.ensure((size_t)(chunk * n_slots * 16)));
     const bool stats = (flags & PRT_FLAG_STATS) != 0;

@@ -4,14 +4,15 @@ The smaller parity tests (test_gpu_parity.py) pin every code path at sizes where
 oracle renders whole frames in seconds.  Here the kernel runs the benchmark workloads
 themselves — the regimes those tests cannot reach:
 
-* config 3 (specular Cornell + glass sphere, 1024^2 x 256 spp, depth 8): two trace
-  launches per frame (the per-sample buffers exceed one chunk);
+* config 3 (specular Cornell + glass sphere, 1024^2 x 256 spp, depth 8): run with the
+  round-1 4 GiB per-launch buffer budget, so the frame takes two equal trace launches
+  (the default 16 GiB budget renders it in one);
 * config 4 (1,000,044-triangle instanced cube.obj, 512^2 x 64 spp, depth 8): the
   global-memory kernel — quantised BVH4 nodes read from HBM, 16-entry LDS stack with
   its global spill area, suspended traversal tails, the drain-aware default variant —
   at a tree depth and stack depth only this scene reaches;
-* config 5 (Cornell 4096^2 x 256 spp, depth 8, on one GPU): 29 chunked launches per
-  frame, a 201 MB result, and prt_render_multi's RCCL self-loop gather of all of it.
+* config 5 (Cornell 4096^2 x 256 spp, depth 8, on one GPU): 8 equal chunked launches per
+  frame (32 spp each), a 201 MB result, and prt_render_multi's RCCL self-loop gather of all of it.
 
 The oracle (oracle/prt_oracle.c) re-renders a seeded random sample of 8x8 tiles of each
 frame at the full spp and depth (its BVH backend: stack traversal of the host-built
@@ -156,10 +157,11 @@ def test_config4_hits_match_oracle(cubes, quantized):
 
 # ----------------------------------------------------------------------------- config 3
 
-def test_config3_full_frame_matches_oracle():
+def test_config3_full_frame_matches_oracle(monkeypatch):
     """1024^2 x 256 spp, depth 8 on the specular scene (metal, dielectric, glass sphere):
-    two trace launches (chunked per-sample buffers); 96 random 8x8 tiles (1.6 M samples)
-    bit-identical to the oracle."""
+    two trace launches of 128 spp (PRT_CHUNK_BYTES = 4 GiB, read at scene creation); 96 random
+    8x8 tiles (1.6 M samples) bit-identical to the oracle."""
+    monkeypatch.setenv("PRT_CHUNK_BYTES", str(4 << 30))
     from test_gpu_parity import _specular_scene
     from pyrenderer_amd.device_scene import DeviceScene
     _, camera, flat = _specular_scene(0.0)
@@ -183,8 +185,8 @@ def config5_frame(gpu_scene, cornell):
 
 
 def test_config5_frame_matches_oracle(gpu_scene, oracle_scene, cornell, config5_frame):
-    """4096^2 x 256 spp, depth 8 (4.29 G samples) on one GPU: 29 chunked trace launches
-    per frame; 64 random 8x8 tiles (1 M samples) bit-identical to the oracle."""
+    """4096^2 x 256 spp, depth 8 (4.29 G samples) on one GPU: 8 chunked trace launches
+    of 32 spp per frame; 64 random 8x8 tiles (1 M samples) bit-identical to the oracle."""
     frame = config5_frame
     assert frame.shape == (4096, 4096, 3)
     assert np.isfinite(frame).all() and (frame >= 0).all()
