@@ -9,7 +9,7 @@ mkdir -p $O
 for c in $CONFIGS; do
   for r in $(seq 1 $ROUNDS); do
     for s in $STREAMS; do
-      timeout -k 10 300 python3 bench.py --config $c --streams $s --steps 30 --no-cpu-baseline --numpy-seconds 0 \
+      timeout -k 10 300 python3 bench.py --config $c --streams $s ${STEPS_ARGS:---steps 30} --no-cpu-baseline --numpy-seconds 0 \
         > $O/c${c}_s${s}_r${r}.json 2> $O/c${c}_s${s}_r${r}.err
       python3 -c "import json; d=json.load(open('$O/c${c}_s${s}_r${r}.json')); print('c$c s$s r$r', round(d['value'],1), round(d['ms_per_step'],3), d['roofline']['kernel_avg_ms'])"
     done
