@@ -96,6 +96,8 @@ def parse():
     ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-primary-kernel", action="store_true",
+                    help="A/B: camera rays generated inside the trace kernel (PRT_FLAG_NO_PRIMARY_KERNEL)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
     ap.add_argument("--numpy-seconds", type=float, default=8.0,
                     help="target wall time of the NumPy-path CPU sample (main.py counterpart); 0 = skip")
@@ -273,7 +275,8 @@ def main():
         n_step[0] += 1
         shard, stream = shards[k], streams[k]
         ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, shard.buf.data_ptr(),
-                               stream.cuda_stream, seed=args.seed, flags=flags | (args.variant << 8))
+                               stream.cuda_stream, seed=args.seed,
+                               flags=flags | (args.variant << 8) | (N.PRT_FLAG_NO_PRIMARY_KERNEL if args.no_primary_kernel else 0))
         with torch.cuda.stream(stream):
             shard.gather()    # RCCL gather of per-tile radiance sums to rank 0 (ordered after this frame)
 
