@@ -693,7 +693,15 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             int stk = variant_stack(s, var);
             s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(stk, var, false, prt::trace_smem_bytes(stk, var, Q)));
         }
-        if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
+        if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) {
+            s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
+        } else {
+            // the default budget takes at most a quarter of the memory free at scene creation (each
+            // render stream holds one such buffer set; 16 GiB of an idle MI355X's 288 GB)
+            size_t free_b = 0, total_b = 0;
+            if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+                s->chunk_bytes = std::max<size_t>((size_t)1 << 28, std::min(s->chunk_bytes, free_b / 4));
+        }
     } while (0);
     if (rc != PRT_OK) { destroy_scene(s); return rc; }
     *out_scene = s;
