@@ -1,6 +1,7 @@
-"""world_size-2 gloo run of the tile-shard + gather path on CPU (the oracle
+"""world_size 2 / 3 / 8 gloo runs of the tile-shard + gather path on CPU (the oracle
 stands in for the GPU renderer): the gathered frame equals the single-process
-frame bit for bit."""
+frame bit for bit — including the driver's N = 8 layout and a frame with fewer tiles
+than ranks (ranks with no tile still join the gather with an empty shard)."""
 import os
 import socket
 
@@ -23,7 +24,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, W=W, H=H):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,10 +47,10 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gather_matches_single_process(tmp_path, world):
+@pytest.mark.parametrize("world, W, H", [(2, W, H), (3, W, H), (8, W, H), (8, 32, 24)])
+def test_gather_matches_single_process(tmp_path, world, W, H):
     out = str(tmp_path / "frame.npy")
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, W, H), nprocs=world, join=True)
     frame = np.load(out)
     from oracle import oracle as O
     from pyrenderer_amd.flatten import flatten_scene
