@@ -906,6 +906,20 @@ void trace_kernel(TraceParams P) {
                 if ((uint64_t)base >= P.n_items) {
                     exhausted = true;
                 } else {
+                    if constexpr (!SCENE_LDS) {
+                        // global scenes: queue chunk c -> (sample c % n, 64-pixel group c / n), so
+                        // the chunks in flight hold every sample of a few pixel groups instead of
+                        // one sample of the whole frame: their paths start (and first bounce) in a
+                        // small part of the scene, and its nodes and triangles stay in L2 (C4
+                        // 18.12 -> 17.51 ms).  LDS scenes keep sample-major chunks, whose staged
+                        // rays and radiance are read and written in address order (pixel-major
+                        // there strides 4 MB per chunk: C2 4.23 -> 4.32 ms; profiles/r02/s5/ab_pm/)
+                        const uint32_t n_samp = (uint32_t)(P.n_items / (uint64_t)P.n_slots);
+                        const uint32_t c = base >> 6;
+                        const uint32_t g = c / n_samp;
+                        base = (c - g * n_samp) * (uint32_t)P.n_slots + (g << 6);
+                        base = __builtin_amdgcn_readfirstlane(base);
+                    }
                     q_next = base;
                     q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
                     if (P.wave_clock && lane == 0)
