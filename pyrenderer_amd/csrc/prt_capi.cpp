@@ -381,11 +381,12 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     // leaves are cheap and traversals short); global scenes enter the leaf phase once at
     // most 16 descending lanes still lack one (C4: 35.1 -> 29.7 ms at 8 in round 1, 18.69 ->
     // 18.44 ms at 16 with leaf exit 12 after the round-2 traversal changes; C2 prefers 0).
-    // Leaf-phase exit: back to descending once at most 8 (LDS) / 12 (global) lanes still
-    // hold a leaf (C2 5.25 -> 5.04 ms in round 1, flat for 8-16 now)
+    // Leaf-phase exit: back to descending once at most 8 (LDS) / 24 (global) lanes still
+    // hold a leaf (C2 5.25 -> 5.04 ms in round 1, flat for 8-16 now; C4 with pixel-major
+    // chunks 17.41 -> 17.22 ms at 24 instead of 12, profiles/r02/s5/knobs_c4_pm/)
     const bool lds_var = prt::variant_uses_lds(var);
     P.leaf_break = s->leaf_break >= 0 ? s->leaf_break : (lds_var ? 0 : 16);
-    P.leaf_exit = s->leaf_exit >= 0 ? s->leaf_exit : (lds_var ? 8 : 12);
+    P.leaf_exit = s->leaf_exit >= 0 ? s->leaf_exit : (lds_var ? 8 : 24);
     int& occ = s->occ[2 * var + (stats ? 1 : 0)];
     if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(stack, var, stats, prt::trace_smem_bytes(stack, var, P)));
     if (spill) {
