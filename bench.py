@@ -94,6 +94,10 @@ def parse():
                     help="frames in flight (1 = strictly serial frames; 0 = auto: 3 when a rank renders < 8 M "
                          "samples per frame, else 2 on several GPUs and 1 on one)")
     ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1: nccl (= RCCL over xGMI, the default) or gloo "
+                         "(tile sums staged through host memory; rehearses the N > 1 path with several ranks "
+                         "on one GPU)")
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-primary-kernel", action="store_true",
@@ -232,13 +236,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; with more ranks than visible GPUs (a gloo rehearsal on a one-GPU box)
+    # ranks share devices round-robin
+    n_dev = max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", local % n_dev if world > 1 else 0)
+    gloo = world > 1 and args.backend == "gloo"
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    coll_dev = torch.device("cpu") if gloo else dev   # where collective operands live
 
     from pyrenderer_amd import _native as N
     from pyrenderer_amd.device_scene import DeviceScene
@@ -266,7 +278,7 @@ def main():
         rank_samples = W * H * args.spp / world
         n_streams = 3 if rank_samples < 8e6 else (2 if world > 1 else 1)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
-    shards = [TileShard(W, H, T, rank, world, dev, args.scheme) for _ in range(n_streams)]
+    shards = [TileShard(W, H, T, rank, world, dev, args.scheme, host_staging=gloo) for _ in range(n_streams)]
     my_tiles = shards[0].tiles
     n_step = [0]
 
@@ -284,7 +296,7 @@ def main():
     step(N.PRT_FLAG_STATS)
     torch.cuda.synchronize(dev)
     st = np.append(ds.last_stats().astype(np.float64), float(ds.diag_stats()[14]))
-    cnt = torch.tensor(st, dtype=torch.float64, device=dev)
+    cnt = torch.tensor(st, dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(cnt)
     nodes, tris, ext, shadow, nonfinite = cnt.tolist()
@@ -305,7 +317,7 @@ def main():
     # the frame is split into chunks of <= PRT chunk bytes of per-sample radiance (several
     # trace launches per step at C5); the roofline is per launch
     launches_per_step = max(launches, 1) / args.steps
-    t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=coll_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_avg_ms = t.tolist()
@@ -352,7 +364,7 @@ def main():
             cpu_np, np_ids, np_sums = numpy_baseline(flat, cam, args, args.numpy_seconds)
             if np_ids is not None:
                 torch.cuda.synchronize(dev)
-                cmp = l2_vs_cpu(shards[0].assemble(), np_ids, np_sums, args)
+                cmp = l2_vs_cpu(shards[0].assemble(ds), np_ids, np_sums, args)
                 cpu_np["l2_vs_gpu"] = {k: cmp[k] for k in ("pixels", "rmse", "max_pixel_l2", "identical_pixels")}
                 # main.py:52's own parallelism (joblib n_jobs=4), on a shorter sample
                 n4, _, _ = numpy_baseline(flat, cam, args, args.numpy_seconds / 2, procs=4)
@@ -364,7 +376,7 @@ def main():
             if world == 1:
                 cpu = cpu_baseline(ids, dt, cores, args)
             torch.cuda.synchronize(dev)
-            l2 = l2_vs_cpu(shards[0].assemble(), ids, cpu_sums, args)
+            l2 = l2_vs_cpu(shards[0].assemble(ds), ids, cpu_sums, args)
         hbm_measured = round(traffic / kern_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
         flops_tf = flops_launch / kern_s / 1e12
         common = {"traffic": traffic, "hbm_measured_frac": hbm_measured, "valu_issue_util": issue,
@@ -411,6 +423,7 @@ def main():
             "config": {"workload": f"{SCENE_NAMES[args.scene]} {W}x{H}, {args.spp} spp, depth {args.depth}",
                        "baseline_config": args.config, "triangles": int(flat.n_tri), "spheres": int(flat.sph.shape[0]),
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
+                       "backend": (args.backend if world > 1 else None),
                        "tile_scheme": args.scheme, "frames_in_flight": n_streams,
                        "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
             "roofline": roofline,
@@ -418,6 +431,9 @@ def main():
                                 "ext_queries": round(ext / samples_per_step, 3),
                                 "shadow_queries": round(shadow / samples_per_step, 3),
                                 "nonfinite_samples": int(nonfinite)},
+            # the same counts summed over the ranks (independent of the tile split for the queries)
+            "work_totals": {"nodes": int(nodes), "tris": int(tris), "ext_queries": int(ext),
+                            "shadow_queries": int(shadow)},
             "cpu_baseline": cpu,
             "cpu_numpy": cpu_np,
             "l2_vs_cpu": l2,

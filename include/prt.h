@@ -28,7 +28,12 @@
 extern "C" {
 #endif
 
-#define PRT_ABI_VERSION 1
+/* ABI 2 (this build): prt_trace_rays, prt_hit_all added; trace-kernel variant ids renumbered
+ * to 1..6 (PRT_FLAG_VARIANT; ABI 1's ids 7..33 are rejected with PRT_ERR_ARG and its 1..6
+ * named other kernels, so a caller built against ABI 1 must check prt_abi_version());
+ * prt_scene_info's info8[4] is the BVH4 LDS traversal stack depth (0: BVH4 too deep for
+ * the LDS-stack variants); watchdog flags are cleared once reported (prt_check_faults). */
+#define PRT_ABI_VERSION 2
 
 #define PRT_OK 0
 #define PRT_ERR_ARG (-1)     /* invalid argument / shape */
@@ -106,7 +111,9 @@ int prt_scene_create(int device,
                      const float* mat, int32_t n_mat,
                      const int32_t* light_tri, const int32_t* light_off, int32_t n_light,
                      const float* direct_rgb, void** out_scene);
-/* info[8] = device, n_tri, n_nodes, bvh depth, stack variant, device bytes, blocks/CU, CUs */
+/* info[8] = device, n_tri, n_nodes, BVH2 depth, BVH4 LDS traversal stack entries (0: the BVH4 is
+ * too deep for the LDS-stack variants, only the spill-stack global variant runs), device
+ * bytes, blocks/CU of the default variant, CUs */
 int prt_scene_info(void* scene, int64_t* info8);
 void prt_scene_destroy(void* scene);
 
@@ -148,6 +155,13 @@ int prt_render(void* scene, const float* cam, int W, int H, int x0, int y0, int 
 int prt_render_multi(void* const* scenes, int n_scenes, const float* cam, int W, int H, int tile, int spp, int depth,
                      uint64_t seed, uint32_t flags, float* out_frame);
 void prt_comm_release(void);
+/* Root side of a one-process-per-GPU gather (pyrenderer_amd.distributed): the
+ * packed tile sums d_packed (device, n_tiles*tw*th x 3 f32, slot order of prt_render_tiles) of the
+ * host tile ids `tile_ids` -> the device frame d_frame (W x H x 3 f32, [x][y]; slots outside the
+ * frame are dropped, pixels of other tiles untouched), one kernel enqueued on `stream` (NULL = the
+ * scene's stream, whose device is used).  Replaces a host-side unpack of the gathered buffers. */
+int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_ids, int n_tiles, int tw, int th,
+                      int W, int H, float* d_frame, void* stream);
 /* Progressive rendering: main_taichi.py:108-127 runs render() once per GUI frame
  * (pixels[x,y] += L, samples[x,y] += 1) and displays the running mean.  This call
  * renders samples first_sample .. first_sample+spp-1 of every pixel (the same
@@ -171,14 +185,15 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
 /* trace-kernel time of every render call made with PRT_FLAG_TIME since the
  * previous prt_kernel_timing() (synchronises on their events, then resets):
  * total ms and number of trace launches.  Also reports PRT_ERR_INTERNAL if the
- * traversal watchdog tripped in the last render (device-output renders are not
- * checked otherwise). */
+ * traversal watchdog tripped in the last render of any stream (and clears the flags,
+ * like prt_check_faults). */
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
 /* Failure detection for renders whose result stays on the device (prt_render_tiles_device,
  * the torch.distributed path): synchronises the device, then reports PRT_ERR_INTERNAL if
  * the traversal watchdog tripped in the last render enqueued on any of this scene's
- * streams (or in the last prt_closest_hits call).  PRT_OK otherwise.  The host-output
- * entry points check the flag themselves. */
+ * streams.  PRT_OK otherwise.  A flag is cleared once reported — by this call, by
+ * prt_kernel_timing, or by the host-output entry points and prt_closest_hits, which check
+ * their own launches — so a fault is never reported against a later, clean render. */
 int prt_check_faults(void* scene);
 /* World.hit_all for a batch of rays (mathematics/intersection_taichi.py:238-291):
  * rays = n x 8 f32 (o.xyz, t_min, d.xyz, t_max); hit_id = original triangle index,
@@ -189,6 +204,24 @@ int prt_check_faults(void* scene);
 #define PRT_HITS_ANY 0x1u
 #define PRT_HITS_QUANTIZED 0x2u
 int prt_closest_hits(void* scene, const float* rays, int64_t n, uint32_t flags, int32_t* hit_id, float* hit_t);
+/* World.hit_all's full 8-tuple for a batch of rays (mathematics/intersection_taichi.py:238-291,
+ * with Quad.hit / Cube.hit's shading at the closest hit, shapes.py:76-110): rays as
+ * prt_closest_hits; out = n x 16 f32 per ray:
+ *   [0] hit_anything (0/1)  [1] t (closest_so_far: t_max on a miss)  [2:5] p = o + t d
+ *   [5:8] normal (flipped toward the ray for two-sided BSDFs, shapes.py:101-102)
+ *   [8] emissive (0/1)  [9:12] attenuation = bsdf.evaluate()  [12:15] scattered direction
+ *   (cosine-hemisphere draw rotated into the normal frame, bsdf.py:29-34)  [15] pdf = |n.wi|/pi
+ * (all zero after [1] on a miss).  The scatter draws 2 numbers from the stream keyed
+ * (seed, ray index, 0) — the reference draws them inside hit_all (shapes.py:105) from
+ * Taichi's stateful RNG, which cannot be reproduced.  Synchronous. */
+int prt_hit_all(void* scene, const float* rays, int64_t n, uint64_t seed, uint32_t flags, float* out16);
+/* PathTracer.trace for caller-supplied rays (core/tracing.py:116-155): the radiance of one
+ * path per ray, depth `depth`.  rays = n x 8 f32 (o.xyz, unused, d.xyz, unused); out_rgb = n x 3
+ * f32.  Ray i draws from the stream keyed (seed, i, 0) — render()'s streams minus the two
+ * camera-jitter draws of main_taichi.py:93-94.  flags: PRT_FLAG_MIS_NEE / PRT_FLAG_VARIANT as for
+ * the render calls.  Runs the persistent trace kernel of prt_render_tiles.  Synchronous. */
+int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_t seed, uint32_t flags,
+                   float* out_rgb);
 /* trace-kernel variant chosen for this scene when flags select none:
  * out4 = {variant, BVH arity (2 or 4), bit 0 scene LDS-resident | bit 1 quantised nodes,
  *         LDS traversal stack entries per lane} */

@@ -83,6 +83,8 @@ def lib():
         L.or_dot_or_zero.argtypes = [_vp, _vp]
         L.or_dot_or_zero.restype = _f
         L.or_direct_mis_scripted.argtypes = [_vp, _vp, _vp, _vp, _vp, _i, _vp]
+        L.or_hit_all_batch.argtypes = [_vp, _i, _i64, _vp, _vp, _vp, _vp, _u64, _vp]
+        L.or_trace_rays.argtypes = [_vp, _i, _i64, _vp, _vp, _i, _u64, _i, _vp]
         _lib = L
     return _lib
 
@@ -162,6 +164,26 @@ class OracleScene:
         nrm = np.zeros((n, 3), np.float32)
         lib().or_closest_batch(self.h, backend, n, _p(ro), _p(rd), _p(t0), _p(t1), _p(hit), _p(t), _p(tri), _p(nrm))
         return hit, t, tri, nrm
+
+    def hit_all(self, ro, rd, tmin, tmax, seed=0, backend=BACKEND_BRUTE):
+        """World.hit_all's 8-tuple per ray as libprt's prt_hit_all: (n, 16) f32 rows = hit, t, p,
+        normal, emit, attenuation, scattered direction, pdf (scatter keyed (seed, i, 0))."""
+        ro = _f32(ro, (-1, 3))
+        rd = _f32(rd, (-1, 3))
+        n = ro.shape[0]
+        t0 = _f32(np.broadcast_to(tmin, (n,)))
+        t1 = _f32(np.broadcast_to(tmax, (n,)))
+        out = np.zeros((n, 16), np.float32)
+        lib().or_hit_all_batch(self.h, backend, n, _p(ro), _p(rd), _p(t0), _p(t1), int(seed), _p(out))
+        return out
+
+    def trace_rays(self, ro, rd, depth, seed=0, backend=BACKEND_BRUTE, nthreads=0):
+        """PathTracer.trace per caller ray as libprt's prt_trace_rays: (n, 3) radiance."""
+        ro = _f32(ro, (-1, 3))
+        rd = _f32(rd, (-1, 3))
+        out = np.zeros((ro.shape[0], 3), np.float32)
+        lib().or_trace_rays(self.h, backend, ro.shape[0], _p(ro), _p(rd), depth, int(seed), nthreads, _p(out))
+        return out
 
     def sample_light_scripted(self, draws):
         d = np.zeros(16, np.float32)

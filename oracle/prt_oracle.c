@@ -772,15 +772,8 @@ static v3 direct_mis(const OScene* s, int backend, v3 p, v3 n, v3 rho, Rng* rng,
     return direct;
 }
 
-/* PathTracer.trace (core/tracing.py:116-155) + render() sample body. */
-static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, int H, int x, int y,
-                       int depth, Rng* rng, int scripted, uint64_t* cnt) {
-    float r0 = rng_next(rng);
-    float u = ((float)x + r0) / (float)(W - 1);
-    float r1 = rng_next(rng);
-    float v = ((float)y + r1) / (float)(H - 1);
-    v3 ro, rd;
-    gen_ray(cam, u, v, rng, &ro, &rd);
+/* PathTracer.trace (core/tracing.py:116-155): the radiance of one path from (ro, rd). */
+static v3 trace_path(const OScene* s, int backend, v3 ro, v3 rd, int depth, Rng* rng, int scripted, uint64_t* cnt) {
     v3 L = mk(0, 0, 0), beta = mk(1, 1, 1);
     v3 lc = mk(s->direct_rgb[0], s->direct_rgb[1], s->direct_rgb[2]);
     for (int b = 0; b < depth; ++b) {
@@ -878,6 +871,18 @@ static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, in
     return L;
 }
 
+/* render() sample body (main_taichi.py:93-97): camera jitter, gen_ray, trace. */
+static v3 trace_sample(const OScene* s, int backend, const float* cam, int W, int H, int x, int y,
+                       int depth, Rng* rng, int scripted, uint64_t* cnt) {
+    float r0 = rng_next(rng);
+    float u = ((float)x + r0) / (float)(W - 1);
+    float r1 = rng_next(rng);
+    float v = ((float)y + r1) / (float)(H - 1);
+    v3 ro, rd;
+    gen_ray(cam, u, v, rng, &ro, &rd);
+    return trace_path(s, backend, ro, rd, depth, rng, scripted, cnt);
+}
+
 /* ------------------------------------------------------------ public API */
 OR_API int or_mt(const float* v0, const float* v1, const float* v2, const float* ro, const float* rd,
                  float t0, float t1, float* t) {
@@ -947,6 +952,52 @@ OR_API void or_closest_batch(void* p, int backend, int64_t n, const float* ro, c
         Hit h = closest_hit(s, backend, ld3(ro + 3 * i), ld3(rd + 3 * i), t0[i], t1[i], NULL);
         out_hit[i] = h.hit; out_t[i] = h.t; out_tri[i] = h.hit ? h.tri : -1;
         st3(out_n + 3 * i, h.hit ? h.n : mk(0, 0, 0));
+    }
+}
+
+/* World.hit_all's 8-tuple for a batch of rays (intersection_taichi.py:238-291; libprt's
+ * prt_hit_all): out16[i] = hit, t (t1 on a miss), p = o + t d, the shading normal (flipped for
+ * two-sided BSDFs, shapes.py:101-102), emit, bsdf.evaluate(), the scattered direction and its pdf
+ * (bsdf.py:29-34 + shapes.py:105-108), the scatter's two draws from the stream keyed
+ * (seed, i, 0); zeros after t on a miss. */
+OR_API void or_hit_all_batch(void* p, int backend, int64_t n, const float* ro, const float* rd, const float* t0,
+                             const float* t1, uint64_t seed, float* out16) {
+    OScene* s = (OScene*)p;
+    for (int64_t i = 0; i < n; ++i) {
+        v3 o = ld3(ro + 3 * i), d = ld3(rd + 3 * i);
+        Hit h = closest_hit(s, backend, o, d, t0[i], t1[i], NULL);
+        float* r = out16 + 16 * i;
+        memset(r, 0, 16 * sizeof(float));
+        r[1] = h.hit ? h.t : t1[i];
+        if (!h.hit) continue;
+        const float* m = mat_of(s, h.tri);
+        Rng rng; memset(&rng, 0, sizeof(rng));
+        rng.state = rng_key(seed, (uint32_t)i, 0u);
+        v3 wi; float pdf;
+        scatter(&rng, h.n, &wi, &pdf);
+        r[0] = 1.0f;
+        st3(r + 2, add(o, scl(d, h.t)));
+        st3(r + 5, h.n);
+        r[8] = m[3] != 0.0f ? 1.0f : 0.0f;
+        r[9] = m[0]; r[10] = m[1]; r[11] = m[2];
+        st3(r + 12, wi);
+        r[15] = pdf;
+    }
+}
+
+/* PathTracer.trace for caller-given rays (libprt's prt_trace_rays): ray i draws from the stream
+ * keyed (seed, i, 0). */
+OR_API void or_trace_rays(void* p, int backend, int64_t n, const float* ro, const float* rd, int depth, uint64_t seed,
+                          int nthreads, float* out) {
+    OScene* s = (OScene*)p;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t i = 0; i < n; ++i) {
+        Rng rng; memset(&rng, 0, sizeof(rng));
+        rng.state = rng_key(seed, (uint32_t)i, 0u);
+        st3(out + 3 * i, trace_path(s, backend, ld3(ro + 3 * i), ld3(rd + 3 * i), depth, &rng, 0, NULL));
     }
 }
 

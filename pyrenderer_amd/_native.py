@@ -10,6 +10,7 @@ import numpy as np
 
 from .build import LIB
 
+ABI_VERSION = 2        # include/prt.h PRT_ABI_VERSION
 PRT_OK = 0
 PRT_ERR_INTERNAL = -6   # device-side check failed (traversal watchdog)
 PRT_FLAG_STATS = 0x1
@@ -56,11 +57,14 @@ EXPORTS = {
     "prt_scene_info": (_i, [_vp, _vp]),
     "prt_scene_kernel": (_i, [_vp, _vp]),
     "prt_closest_hits": (_i, [_vp, _vp, ctypes.c_int64, _u32, _vp, _vp]),
+    "prt_hit_all": (_i, [_vp, _vp, _i64, _u64, _u32, _vp]),
+    "prt_trace_rays": (_i, [_vp, _vp, _i64, _i, _u64, _u32, _vp]),
     "prt_scene_destroy": (None, [_vp]),
     "prt_render_tiles": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_multi": (_i, [_vp, _i, _vp, _i, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_comm_release": (None, []),
+    "prt_scatter_tiles": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_tiles_accumulate": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_kernel_timing": (_i, [_vp, _vp, _vp]),
@@ -90,7 +94,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.prt_abi_version() != 1:
+        if L.prt_abi_version() != ABI_VERSION:
             raise PrtError(-101, "ABI version mismatch")
         _lib = L
     return _lib

@@ -17,7 +17,9 @@ SOURCES = ["prt_kernels.hip", "prt_capi.cpp", "prt_bvh.cpp"]
 # the persistent trace kernel's instantiation sets: prt_trace_inst.hip compiled once
 # per (traversal stack entries, stats) pair — the objects build in parallel
 TRACE_INST = "prt_trace_inst.hip"
-TRACE_SETS = [(s, t) for s in (4, 10, 16, 32, 64) for t in (0, 1)]
+# stacks: 4 (the spill test's LDS part), 10 / 16 (LDS-resident scenes, the global scene's LDS
+# part), 32 (deeper LDS-resident BVHs, PRT_SPILL_LDS=32)
+TRACE_SETS = [(s, t) for s in (4, 10, 16, 32) for t in (0, 1)]
 HEADERS = ["prt_kernels.h", "prt_internal.h", "prt_device.h"]
 OBJ_DIR = os.path.join(LIB_DIR, "obj")
 ARCH = os.environ.get("PRT_OFFLOAD_ARCH", "gfx950")

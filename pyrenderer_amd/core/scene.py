@@ -4,6 +4,8 @@ Holds primitives and lights in insertion order and the concatenated
 vertices/faces, as the reference does.  The CPU `hit`/BVH helpers of the
 reference's NumPy debug stack are out of scope.
 """
+import random
+
 import numpy as np
 
 
@@ -29,4 +31,9 @@ class Scene:
             self.faces = np.vstack([self.faces, prim.faces + increment])
 
     def sample_light(self):
-        raise NotImplementedError("light sampling runs in the HIP kernel (core.tracing.render)")
+        """A point on a random light (core/scene.py:23-28: random.choice(lights).sample_a_point()).
+        Host-side debug API of the reference's NumPy stack; the renderer samples lights on the GPU."""
+        if len(self.lights) > 0:
+            return random.choice(self.lights).sample_a_point()
+        print("[WARNING] no lights found")
+        return None

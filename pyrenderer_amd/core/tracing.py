@@ -29,14 +29,28 @@ from ..mathematics.intersection import World
 
 
 class PathTracer:
-    """Same constructor as the reference; `trace` is per-sample GPU work, so
-    the usable entry point is `render_sums` / `render`."""
+    """Same constructor as the reference (core/tracing.py:47-50).  `trace` runs the reference's
+    per-ray estimator for a batch of caller rays; `render_sums` / `render` run render()'s
+    per-pixel sample loop (main_taichi.py:80-99) over the whole frame."""
 
     def __init__(self, world, depth, img_w, img_h):
         self.world = world
         self.depth = depth
         self.img_w = img_w
         self.img_h = img_h
+
+    def trace(self, ro, rd, depth=None, x=None, y=None, *, seed=0, device=0, nee="reference"):
+        """PathTracer.trace (core/tracing.py:116-155) on the GPU: the radiance of one path per ray,
+        for one ray ((3,) arrays) or a batch ((n, 3) arrays), as float32 (3,) / (n, 3).
+
+        depth defaults to the constructor's.  x, y are accepted for the reference's signature
+        (its trace ignores them).  Ray i draws from the random stream keyed (seed, i, 0): the
+        streams render() uses minus the two camera-jitter draws (include/prt.h prt_trace_rays)."""
+        o = np.asarray(ro, np.float32)
+        single = o.ndim == 1
+        ds = self.world.device_scene(device)
+        out = ds.trace_rays(o, rd, self.depth if depth is None else int(depth), seed=seed, flags=nee_flags(nee))
+        return out[0] if single else out
 
     def render_sums(self, cam_packed, spp, seed=0, devices=(0,), tile=64, flags=0):
         """Per-pixel radiance SUMS over spp samples, (W, H, 3) [x][y]."""

@@ -277,12 +277,16 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     if (const char* e = std::getenv("PRT_ESC_BETA")) esc_beta = std::max(0.0, std::atof(e));
     std::vector<int32_t> ref_tri;
     ref_tri.reserve((size_t)n_tri);
-    const int64_t ref_cap = 2 * n_tri + 4096;
+    // the cap stays below the 2^27 references the leaf encoding addresses: past it every further
+    // triangle keeps one reference (a scene with < 2^27 triangles always builds)
+    const int64_t ref_cap = std::min<int64_t>(2 * n_tri + 4096, ((int64_t)1 << 27) - 1);
     std::vector<RefBox> pieces;
     for (int64_t i = 0; i < n_tri; ++i) {
         const Box& b = tri_box[(size_t)i];
         pieces.clear();
-        if (esc_beta > 0.0 && b.area() > esc_beta * mean_area && (int64_t)B.tb.size() < ref_cap) {
+        // mean_area > 0: a scene of degenerate boxes (area 0) would split every other triangle
+        // to the maximum depth against a zero threshold
+        if (esc_beta > 0.0 && mean_area > 0.0 && b.area() > esc_beta * mean_area && (int64_t)B.tb.size() < ref_cap) {
             const float* t = tri_v + 9 * i;
             double v[3][3];
             for (int a = 0; a < 3; ++a)
@@ -291,7 +295,8 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
             for (int k = 0; k < 3; ++k) { cell.lo[k] = b.lo[k]; cell.hi[k] = b.hi[k]; }
             split_refs(v, cell, esc_beta * mean_area, 0, &pieces);
         }
-        if (pieces.size() <= 1) {
+        // one triangle yields up to 2^12 pieces: past the remaining budget it keeps one reference
+        if (pieces.size() <= 1 || (int64_t)(B.tb.size() + pieces.size() + (size_t)(n_tri - i - 1)) > ref_cap) {
             B.tb.push_back(b);
             ref_tri.push_back((int32_t)i);
         } else {
@@ -436,13 +441,17 @@ inline double child_area(const Child& c) {
 void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
     // Each BVH4 node takes a BVH2 node's two children and repeatedly opens the
     // inner child with the largest surface area until it holds four children.
-    struct Item { int32_t b2node; int32_t slot; int32_t depth; };
+    // anc = entries the traversal can hold for the node's strict ancestors: a visit continues
+    // with one hit child and pushes the others (<= children - 1), and LIFO order means the
+    // stack below a node holds only siblings of its ancestors (traverse_ww4)
+    struct Item { int32_t b2node; int32_t slot; int32_t depth; int32_t anc; };
     std::vector<Item> work;
     out->nodes.clear();
     out->nodes.resize(32, 0.0f);
     out->n_nodes = 1;
     out->depth = 0;
-    work.push_back({0, 0, 0});
+    int32_t max_anc = 0;
+    work.push_back({0, 0, 0, 0});
     while (!work.empty()) {
         Item it = work.back();
         work.pop_back();
@@ -481,7 +490,7 @@ void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
                     ref = (int32_t)out->n_nodes++;
                     out->nodes.resize((size_t)out->n_nodes * 32, 0.0f);
                     f = out->nodes.data() + (size_t)it.slot * 32;   // storage may have moved
-                    work.push_back({ch[k].ref, ref, it.depth + 1});
+                    work.push_back({ch[k].ref, ref, it.depth + 1, it.anc + (int32_t)ch.size() - 1});
                 } else {
                     ref = ch[k].ref;
                 }
@@ -489,8 +498,11 @@ void collapse_bvh4(const BvhHost& b2, Bvh4Host* out) {
             std::memcpy(f + 24 + k, &ref, 4);
         }
         out->depth = std::max(out->depth, it.depth);
+        max_anc = std::max(max_anc, it.anc);
     }
-    out->stack_need = 3 * (out->depth + 1) + 1;
+    // the sentinel, the deepest node's ancestor entries, and the <= 3 slots a visit writes
+    // above the top unconditionally (visit_node4); <= 3 (depth + 1) + 1, the per-level bound
+    out->stack_need = 1 + max_anc + 3;
 }
 
 void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out) {

@@ -139,6 +139,11 @@ struct Scene {
     // of every rank and their tile origins (host copy kept alive for the async upload)
     DevBuf frame, gather, gather_xy;
     std::vector<uint32_t> gather_xy_host;
+    // prt_scatter_tiles: tile origins of the last call (host copy alive until its upload has run,
+    // i.e. until scatter_ev completes)
+    DevBuf scatter_xy;
+    std::vector<uint32_t> scatter_xy_host;
+    hipEvent_t scatter_ev = nullptr;
 };
 
 struct DeviceGuard {
@@ -159,13 +164,14 @@ void destroy_scene(Scene* s) {
     DeviceGuard g(s->device);
     for (DevBuf* b : {&s->nodes4q, &s->nodes4, &s->tris, &s->tri_nm, &s->tri_frame, &s->mats, &s->light_v,
                       &s->light_off, &s->sph, &s->sph_mat, &s->work, &s->stats, &s->frame, &s->gather,
-                      &s->gather_xy})
+                      &s->gather_xy, &s->scatter_xy})
         b->release();
     if (!s->ctx.empty()) (void)hipDeviceSynchronize();
     for (auto& c : s->ctx)
         for (DevBuf* b : {&c->tiles, &c->buf, &c->rays, &c->work, &c->acc, &c->spill})
             b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
+    if (s->scatter_ev) (void)hipEventDestroy(s->scatter_ev);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
@@ -191,18 +197,24 @@ int check_render_args(Scene* s, const float* cam, int W, int H, int tw, int th, 
 // work.p: [0] chunk counter; [kFaultOffset] traversal watchdog flag
 constexpr size_t kFaultOffset = 32;
 
-int read_fault_at(const DevBuf& work) {
+// Reads a watchdog flag and clears it once read, so every fault is reported exactly once:
+// by the call whose launch raised it (host-output renders, hit queries), or by the first
+// prt_check_faults / prt_kernel_timing after a device-output render.  A flag left set would
+// otherwise be reported against every later, clean render (callers synchronise first).
+int take_fault_at(const DevBuf& work) {
     int f = 0;
     if (!work.p) return 0;
     if (hipMemcpy(&f, (char*)work.p + kFaultOffset, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (f != 0 && hipMemset((char*)work.p + kFaultOffset, 0, sizeof(int)) != hipSuccess) return -1;
     return f;
 }
-int read_fault(Scene* s) { return read_fault_at(s->work); }
-// any render context's watchdog flag (callers synchronise first)
-int read_render_faults(Scene* s) {
+int take_fault(Scene* s) { return take_fault_at(s->work); }
+// every render context's watchdog flag (all are taken, not only the first one set)
+int take_render_faults(Scene* s) {
+    int any = 0;
     for (auto& c : s->ctx)
-        if (int f = read_fault_at(c->work)) return f;
-    return 0;
+        if (int f = take_fault_at(c->work)) any = any ? any : f;
+    return any;
 }
 
 // The render context of `stream`, created on first use.  Beyond kMaxCtx streams the
@@ -274,6 +286,72 @@ bool camera_is_fast(const float* cam) {
     return fin && !(cam[19] > 0.0f) && cam[12] == 0.0f && cam[13] == 0.0f && cam[14] == 0.0f && cam[15] == 1.0f;
 }
 
+// Scene part of a trace launch's parameters (everything but the work description).
+void scene_params(Scene* s, prt::TraceParams& P) {
+    std::memset(&P, 0, sizeof(P));
+    P.nodes = (const float4*)s->nodes4.p;
+    P.tris = (const float4*)s->tris.p;
+    P.tri_nm = (const float4*)s->tri_nm.p;
+    P.tri_frame = (const float4*)s->tri_frame.p;
+    P.mats = (const float*)s->mats.p;
+    P.light_v = (const float4*)s->light_v.p;
+    P.light_off = (const int*)s->light_off.p;
+    P.n_light = s->n_light;
+    P.dl_r = s->direct_rgb[0]; P.dl_g = s->direct_rgb[1]; P.dl_b = s->direct_rgb[2];
+    P.resume_min = s->resume_min;
+    P.stats = (unsigned long long*)s->stats.p;
+    scene_sizes(s, P);
+    P.guard_trips = s->guard_trips;
+    P.n_sph = (int)s->n_sph;
+    P.sph = (const float4*)s->sph.p;
+    P.sph_mat = (const int*)s->sph_mat.p;
+}
+
+// Kernel variant (flags or the scene's default), its traversal stack, the blocks per CU of
+// the persistent grid and the spill area of the global variants; switches P to the quantised
+// nodes for the variants that read them.
+int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, prt::TraceParams& P, int* var_out, int* stack_out,
+                int* occ_out) {
+    const bool stats = (flags & PRT_FLAG_STATS) != 0;
+    int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFFu);
+    const bool mis = (flags & PRT_FLAG_MIS_NEE) != 0;
+    if (var == 0) var = !mis ? default_variant(s) : (lds_fits4(s) && s->stack4) ? prt::kVarLdsMis : prt::kVarGlobalMis;
+    if (var < prt::kVarFirst || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
+    if (prt::variant_mis(var) != mis)
+        return fail(PRT_ERR_ARG, "PRT_FLAG_MIS_NEE must be set exactly for the MIS estimator variants");
+    const bool spill = prt::variant_spills(var);
+    if (s->stack4 == 0 && !spill) return fail(PRT_ERR_ARG, "BVH4 too deep for the LDS traversal stack variants");
+    const int stack = variant_stack(s, var);
+    if (prt::variant_quantized(var)) {
+        P.nodes = (const float4*)s->nodes4q.p;
+        P.n_node_f4 = (int)s->n_node4q_f4;
+    }
+    if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
+    // while-while leaf-phase entry: LDS scenes wait for every descending lane's leaf (their
+    // leaves are cheap and traversals short); global scenes enter the leaf phase once at
+    // most 16 descending lanes still lack one (C4: 35.1 -> 29.7 ms at 8 in round 1, 18.69 ->
+    // 18.44 ms at 16 with leaf exit 12 after the round-2 traversal changes; C2 prefers 0).
+    // Leaf-phase exit: back to descending once at most 8 (LDS) / 24 (global) lanes still
+    // hold a leaf (C2 5.25 -> 5.04 ms in round 1, flat for 8-16 now; C4 with pixel-major
+    // chunks 17.37-17.46 ms at 24 against 17.50-17.64 at 12 in three interleaved rounds,
+    // profiles/r03/s1_baseline/leafexit/)
+    const bool lds_var = prt::variant_uses_lds(var);
+    P.leaf_break = s->leaf_break >= 0 ? s->leaf_break : (lds_var ? 0 : 16);
+    P.leaf_exit = s->leaf_exit >= 0 ? s->leaf_exit : (lds_var ? 8 : 24);
+    int& occ = s->occ[2 * var + (stats ? 1 : 0)];
+    if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(stack, var, stats, prt::trace_smem_bytes(stack, var, P)));
+    if (spill) {
+        // entries [spill_lds, need4] of every lane of the largest grid, plus one slot of headroom
+        size_t per_lane = (size_t)std::max(1, s->need4 + 2 - s->spill_lds);
+        HIP_TRY(cx->spill.ensure(per_lane * (size_t)occ * s->cus * 256 * sizeof(int)));
+        P.spill = (int*)cx->spill.p;
+    }
+    *var_out = var;
+    *stack_out = stack;
+    *occ_out = occ;
+    return PRT_OK;
+}
+
 // Enqueue the whole render of a tile set on `stream`, result in d_acc: samples
 // first_sample .. first_sample + spp - 1 of every pixel; `accumulate` adds them onto the
 // sums already in d_acc (progressive rendering) instead of overwriting them.
@@ -307,7 +385,19 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     const bool primary = cam_fast && !(flags & PRT_FLAG_NO_PRIMARY_KERNEL);
     int64_t per_sample = n_slots * 3 * (int64_t)sizeof(float);
     int64_t per_sample_all = per_sample + (primary ? n_slots * 16 : 0);
-    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)s->chunk_bytes / per_sample_all));
+    // per-launch budget: the scene's (<= 16 GiB), and when this context's buffers must grow, at
+    // most half of the device memory free now plus what they already hold — every render stream
+    // (up to kMaxCtx) owns such a buffer set, so a budget fixed at scene creation could ask
+    // several streams' worth of the memory that was free then
+    size_t budget = s->chunk_bytes;
+    {
+        const size_t held = cx->buf.bytes + cx->rays.bytes;
+        size_t free_b = 0, total_b = 0;
+        if ((size_t)(std::min<int64_t>(spp, (int64_t)(budget / (size_t)per_sample_all)) * per_sample_all) > held &&
+            hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+            budget = std::min(budget, std::max<size_t>((size_t)per_sample_all, (free_b + held) / 2));
+    }
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)budget / per_sample_all));
     // keep every chunk's item count below 2^31 (32-bit work counter)
     chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, ((int64_t)1 << 31) / n_slots - 1));
     // equal launches: no short last launch paying a whole launch tail for a few samples
@@ -324,20 +414,10 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     if (!primary) HIP_TRY(hipMemsetAsync((char*)cx->work.p + kFaultOffset, 0, sizeof(int), stream));
 
     prt::TraceParams P;
-    std::memset(&P, 0, sizeof(P));
-    P.nodes = (const float4*)s->nodes4.p;
-    P.tris = (const float4*)s->tris.p;
-    P.tri_nm = (const float4*)s->tri_nm.p;
-    P.tri_frame = (const float4*)s->tri_frame.p;
-    P.mats = (const float*)s->mats.p;
-    P.light_v = (const float4*)s->light_v.p;
-    P.light_off = (const int*)s->light_off.p;
-    P.n_light = s->n_light;
-    P.dl_r = s->direct_rgb[0]; P.dl_g = s->direct_rgb[1]; P.dl_b = s->direct_rgb[2];
+    scene_params(s, P);
     std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
     {
         P.cam_fast = cam_fast ? 1 : 0;
-        P.resume_min = s->resume_min;
         P.rays = primary ? (const float4*)cx->rays.p : nullptr;
         const float rd2 = -cam[18];
         for (int i = 0; i < 3; ++i) {
@@ -357,45 +437,8 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     P.work = (uint32_t*)cx->work.p;
     P.fault = (int*)((char*)cx->work.p + kFaultOffset);
     P.out = (float*)cx->buf.p;
-    P.stats = (unsigned long long*)s->stats.p;
-    scene_sizes(s, P);
-    P.guard_trips = s->guard_trips;
-    P.n_sph = (int)s->n_sph;
-    P.sph = (const float4*)s->sph.p;
-    P.sph_mat = (const int*)s->sph_mat.p;
-    int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFFu);
-    const bool mis = (flags & PRT_FLAG_MIS_NEE) != 0;
-    if (var == 0) var = !mis ? default_variant(s) : (lds_fits4(s) && s->stack4) ? prt::kVarLdsMis : prt::kVarGlobalMis;
-    if (var < prt::kVarFirst || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
-    if (prt::variant_mis(var) != mis)
-        return fail(PRT_ERR_ARG, "PRT_FLAG_MIS_NEE must be set exactly for the MIS estimator variants");
-    const bool spill = prt::variant_spills(var);
-    if (s->stack4 == 0 && !spill) return fail(PRT_ERR_ARG, "BVH4 too deep for the LDS traversal stack variants");
-    const int stack = variant_stack(s, var);
-    if (prt::variant_quantized(var)) {
-        P.nodes = (const float4*)s->nodes4q.p;
-        P.n_node_f4 = (int)s->n_node4q_f4;
-    }
-    if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
-    // while-while leaf-phase entry: LDS scenes wait for every descending lane's leaf (their
-    // leaves are cheap and traversals short); global scenes enter the leaf phase once at
-    // most 16 descending lanes still lack one (C4: 35.1 -> 29.7 ms at 8 in round 1, 18.69 ->
-    // 18.44 ms at 16 with leaf exit 12 after the round-2 traversal changes; C2 prefers 0).
-    // Leaf-phase exit: back to descending once at most 8 (LDS) / 24 (global) lanes still
-    // hold a leaf (C2 5.25 -> 5.04 ms in round 1, flat for 8-16 now; C4 with pixel-major
-    // chunks 17.41 -> 17.22 ms at 24 instead of 12, profiles/r02/s5/knobs_c4_pm/)
-    const bool lds_var = prt::variant_uses_lds(var);
-    P.leaf_break = s->leaf_break >= 0 ? s->leaf_break : (lds_var ? 0 : 16);
-    P.leaf_exit = s->leaf_exit >= 0 ? s->leaf_exit : (lds_var ? 8 : 24);
-    int& occ = s->occ[2 * var + (stats ? 1 : 0)];
-    if (occ == 0) occ = std::max(1, prt::trace_blocks_per_cu(stack, var, stats, prt::trace_smem_bytes(stack, var, P)));
-    if (spill) {
-        // entries [spill_lds, need4] of every lane of the largest grid, plus one slot of headroom
-        size_t per_lane = (size_t)std::max(1, s->need4 + 2 - s->spill_lds);
-        HIP_TRY(cx->spill.ensure(per_lane * (size_t)occ * s->cus * 256 * sizeof(int)));
-        P.spill = (int*)cx->spill.p;
-    }
-
+    int var = 0, stack = 0, occ = 0;
+    if (int rc = trace_setup(s, cx, flags, P, &var, &stack, &occ)) return rc;
     int64_t n_chunks = (spp + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
     int k = s->ev_used / 2;
@@ -649,7 +692,7 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             prt::collapse_bvh4(bvh, &b4);
             s->depth4 = b4.depth;
             s->n_node4_f4 = (int64_t)b4.nodes.size() / 4;
-            s->stack4 = b4.stack_need <= 64 ? prt::stack_variant(b4.stack_need - 1) : 0;
+            s->stack4 = b4.stack_need <= 32 ? prt::stack_variant(b4.stack_need - 1) : 0;
             s->need4 = b4.stack_need;
             if ((rc = upload(s->nodes4, b4.nodes.data(), sizeof(float) * b4.nodes.size(), &s->device_bytes))) break;
             std::vector<float> q4;
@@ -697,8 +740,9 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         if (const char* cb = std::getenv("PRT_CHUNK_BYTES")) {
             s->chunk_bytes = (size_t)std::max(1LL << 20, std::atoll(cb));
         } else {
-            // the default budget takes at most a quarter of the memory free at scene creation (each
-            // render stream holds one such buffer set; 16 GiB of an idle MI355X's 288 GB)
+            // the default budget takes at most a quarter of the memory free at scene creation (16 GiB
+            // of an idle MI355X's 288 GB); enqueue_render also caps it by the memory free when a
+            // render stream's buffers grow
             size_t free_b = 0, total_b = 0;
             if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
                 s->chunk_bytes = std::max<size_t>((size_t)1 << 28, std::min(s->chunk_bytes, free_b / 4));
@@ -744,7 +788,103 @@ int prt_closest_hits(void* scene, const float* rays, int64_t n, uint32_t flags, 
     HIP_TRY(hipMemcpyAsync(hit_id, d_id.p, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipMemcpyAsync(hit_t, d_t.p, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if (read_fault(s) != 0) return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
+    if (take_fault(s) != 0) return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
+    return PRT_OK;
+}
+
+int prt_hit_all(void* scene, const float* rays, int64_t n, uint64_t seed, uint32_t flags, float* out16) {
+    auto* s = (Scene*)scene;
+    if (!s || (n > 0 && (!rays || !out16))) return fail(PRT_ERR_ARG, "NULL argument");
+    if (n < 0) return fail(PRT_ERR_ARG, "n < 0");
+    if (flags & ~PRT_HITS_QUANTIZED) return fail(PRT_ERR_ARG, "prt_hit_all takes only PRT_HITS_QUANTIZED");
+    if (n == 0) return PRT_OK;
+    if (s->need4 > 64) return fail(PRT_ERR_ARG, "BVH4 too deep for the hit-query kernel");
+    DeviceGuard g(s->device);
+    const bool quant = (flags & PRT_HITS_QUANTIZED) != 0;
+    prt::TraceParams P;
+    scene_params(s, P);
+    if (quant) P.nodes = (const float4*)s->nodes4q.p;
+    P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
+    P.fault = (int*)((char*)s->work.p + kFaultOffset);
+    DevBuf d_rays, d_id, d_t, d_out;
+    HIP_TRY(d_rays.ensure(sizeof(float) * 8 * (size_t)n));
+    HIP_TRY(d_id.ensure(sizeof(int32_t) * (size_t)n));
+    HIP_TRY(d_t.ensure(sizeof(float) * (size_t)n));
+    HIP_TRY(d_out.ensure(sizeof(float) * 16 * (size_t)n));
+    HIP_TRY(hipMemsetAsync(P.fault, 0, sizeof(int), s->stream));
+    HIP_TRY(hipMemcpyAsync(d_rays.p, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(prt::launch_hits(P, quant, false, 64, (const float4*)d_rays.p, n, (int*)d_id.p, (float*)d_t.p, s->stream));
+    HIP_TRY(prt::launch_hit_shade(P, (const float4*)d_rays.p, n, (const int*)d_id.p, (const float*)d_t.p,
+                                  (float*)d_out.p, s->stream));
+    HIP_TRY(hipMemcpyAsync(out16, d_out.p, sizeof(float) * 16 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (take_fault(s) != 0) return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
+    return PRT_OK;
+}
+
+int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_t seed, uint32_t flags,
+                   float* out_rgb) {
+    auto* s = (Scene*)scene;
+    if (!s || (n > 0 && (!rays || !out_rgb))) return fail(PRT_ERR_ARG, "NULL argument");
+    if (n < 0 || depth < 0) return fail(PRT_ERR_ARG, "n and depth must be >= 0");
+    if (flags & (PRT_FLAG_NO_PRIMARY_KERNEL | PRT_FLAG_TIME))
+        return fail(PRT_ERR_ARG, "prt_trace_rays: PRT_FLAG_NO_PRIMARY_KERNEL / PRT_FLAG_TIME do not apply");
+    if (n == 0) return PRT_OK;
+    if (n >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many rays in one call (< 2^31)");
+    DeviceGuard g(s->device);
+    if (depth == 0) {
+        std::memset(out_rgb, 0, sizeof(float) * 3 * (size_t)n);
+        return PRT_OK;
+    }
+    RenderCtx* cx = ctx_for(s, s->stream);
+    if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
+    // the rays as one "sample" of a frame of 64 x 1 tiles: item = slot = ray index (every chunk
+    // of 64 items one tile); the trace kernel's tile origins are (0, tile)
+    constexpr int64_t kRowRays = 64;
+    const int64_t n_pad = (n + kRowRays - 1) / kRowRays * kRowRays;
+    const int64_t n_tiles = n_pad / kRowRays;
+    if (n_tiles > 65535) return fail(PRT_ERR_ARG, "too many rays in one call (<= 65535 x 64)");
+    std::vector<uint32_t> origins((size_t)n_tiles);
+    for (int64_t t = 0; t < n_tiles; ++t) origins[(size_t)t] = (uint32_t)t;
+    HIP_TRY(cx->tiles.ensure(sizeof(uint32_t) * (size_t)n_tiles));
+    HIP_TRY(hipMemcpy(cx->tiles.p, origins.data(), sizeof(uint32_t) * (size_t)n_tiles, hipMemcpyHostToDevice));
+    cx->tile_host.clear();   // the next tile render re-uploads its own origins
+    DevBuf d_in, d_org, d_out;
+    HIP_TRY(d_in.ensure(sizeof(float) * 8 * (size_t)n));
+    HIP_TRY(d_org.ensure(sizeof(float) * 4 * (size_t)n_pad));
+    HIP_TRY(d_out.ensure(sizeof(float) * 3 * (size_t)n_pad));
+    HIP_TRY(cx->rays.ensure(sizeof(float) * 4 * (size_t)n_pad));
+    HIP_TRY(hipMemcpyAsync(d_in.p, rays, sizeof(float) * 8 * (size_t)n, hipMemcpyHostToDevice, s->stream));
+    prt::TraceParams P;
+    scene_params(s, P);
+    P.rays = (const float4*)cx->rays.p;
+    P.ray_o = (const float4*)d_org.p;
+    P.W = (int)kRowRays; P.H = (int)n_tiles;
+    P.wm1 = (float)(kRowRays - 1); P.hm1 = (float)std::max<int64_t>(n_tiles - 1, 1);
+    P.log_tw = 6;
+    P.log_tpx = 6;
+    P.tile_xy = (const uint32_t*)cx->tiles.p;
+    P.n_slots = (int)n_pad;
+    P.s0 = 0;
+    P.n_items = (uint64_t)n_pad;
+    P.depth = depth;
+    P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
+    P.work = (uint32_t*)cx->work.p;
+    P.fault = (int*)((char*)cx->work.p + kFaultOffset);
+    P.out = (float*)d_out.p;
+    int var = 0, stack = 0, occ = 0;
+    if (int rc = trace_setup(s, cx, flags, P, &var, &stack, &occ)) return rc;
+    const bool stats = (flags & PRT_FLAG_STATS) != 0;
+    if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), s->stream));
+    HIP_TRY(hipMemsetAsync(cx->work.p, 0, 64, s->stream));   // work counter and watchdog flag
+    HIP_TRY(prt::launch_rays_prep(P, (const float*)d_in.p, n, n_pad, (float4*)cx->rays.p, (float4*)d_org.p, s->stream));
+    const int64_t blocks_needed = (n_pad + 255) / 256;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
+    HIP_TRY(prt::launch_trace(P, stack, var, grid, stats, s->stream));
+    HIP_TRY(hipMemcpyAsync(out_rgb, d_out.p, sizeof(float) * 3 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (take_fault_at(cx->work) != 0)
+        return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     return PRT_OK;
 }
 
@@ -777,7 +917,7 @@ int prt_render_tiles(void* scene, const float* cam, int W, int H, int tw, int th
     if (n_slots)
         HIP_TRY(hipMemcpyAsync(out_sum, cx->acc.p, sizeof(float) * 3 * (size_t)n_slots, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if (read_fault_at(cx->work) != 0)
+    if (take_fault_at(cx->work) != 0)
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     if (stats) {
         if (flags & PRT_FLAG_STATS) {
@@ -813,7 +953,7 @@ int prt_render_tiles_accumulate(void* scene, const float* cam, int W, int H, int
         return rc;
     HIP_TRY(hipMemcpyAsync(io_sum, cx->acc.p, bytes, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if (read_fault_at(cx->work) != 0)
+    if (take_fault_at(cx->work) != 0)
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     return PRT_OK;
 }
@@ -844,7 +984,7 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
     }
     *ms_total = tot;
     *launches = s->ev_used / 2;
-    if (read_render_faults(s) != 0) {
+    if (take_render_faults(s) != 0) {
         s->ev_used = 0;
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     }
@@ -859,7 +999,7 @@ int prt_check_faults(void* scene) {
     // every stream a render was enqueued on: the device-wide synchronisation also covers
     // streams the caller owns (torch streams) without holding their handles past their life
     HIP_TRY(hipDeviceSynchronize());
-    if (read_render_faults(s) != 0 || read_fault(s) != 0)
+    if ((take_render_faults(s) | take_fault(s)) != 0)
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     return PRT_OK;
 }
@@ -924,7 +1064,7 @@ int prt_render(void* scene, const float* cam, int W, int H, int x0, int y0, int 
                                 h, (float*)s->frame.p, s->stream));
     HIP_TRY(hipMemcpyAsync(out_sum, s->frame.p, out_bytes, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if (read_fault_at(cx->work) != 0)
+    if (take_fault_at(cx->work) != 0)
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     if (stats) {
         std::memset(stats, 0, 4 * sizeof(uint64_t));
@@ -934,6 +1074,39 @@ int prt_render(void* scene, const float* cam, int W, int H, int x0, int y0, int 
             for (int i = 0; i < 4; ++i) stats[i] = hs[i];
         }
     }
+    return PRT_OK;
+}
+
+int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_ids, int n_tiles, int tw, int th,
+                      int W, int H, float* d_frame, void* stream) {
+    auto* s = (Scene*)scene;
+    if (!s) return fail(PRT_ERR_ARG, "scene is NULL");
+    if (n_tiles < 0 || (n_tiles > 0 && (!tile_ids || !d_packed || !d_frame))) return fail(PRT_ERR_ARG, "NULL argument");
+    if (tw < 1 || th < 1 || (tw & (tw - 1)) || (th & (th - 1)) || (int64_t)tw * th > (1 << 20))
+        return fail(PRT_ERR_ARG, "tile width/height must be powers of two with tw*th <= 2^20");
+    if (W < 1 || H < 1 || W > 65535 || H > 65535) return fail(PRT_ERR_ARG, "frame must be 1..65535 pixels per side");
+    const int tiles_x = (W + tw - 1) / tw, tiles_y = (H + th - 1) / th;
+    for (int i = 0; i < n_tiles; ++i)
+        if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y)
+            return fail(PRT_ERR_ARG, "tile id out of range: " + std::to_string(tile_ids[i]));
+    if ((int64_t)n_tiles * tw * th >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many slots in one call");
+    if (n_tiles == 0) return PRT_OK;
+    DeviceGuard g(s->device);
+    hipStream_t st = stream ? (hipStream_t)stream : s->stream;
+    // the previous call's upload must have run before its host copy / device buffer are reused
+    if (s->scatter_ev) HIP_TRY(hipEventSynchronize(s->scatter_ev));
+    else HIP_TRY(hipEventCreateWithFlags(&s->scatter_ev, hipEventDisableTiming));
+    s->scatter_xy_host.resize((size_t)n_tiles);
+    for (int i = 0; i < n_tiles; ++i)
+        s->scatter_xy_host[(size_t)i] =
+            ((uint32_t)((tile_ids[i] % tiles_x) * tw) << 16) | (uint32_t)((tile_ids[i] / tiles_x) * th);
+    HIP_TRY(s->scatter_xy.ensure(sizeof(uint32_t) * (size_t)n_tiles));
+    HIP_TRY(hipMemcpyAsync(s->scatter_xy.p, s->scatter_xy_host.data(), sizeof(uint32_t) * (size_t)n_tiles,
+                           hipMemcpyHostToDevice, st));
+    const int log_tw = __builtin_ctz((unsigned)tw), log_tpx = __builtin_ctz((unsigned)(tw * th));
+    HIP_TRY(prt::launch_scatter(d_packed, (const uint32_t*)s->scatter_xy.p, n_tiles * tw * th, log_tw, log_tpx, 0, 0, W,
+                                H, d_frame, st));
+    HIP_TRY(hipEventRecord(s->scatter_ev, st));
     return PRT_OK;
 }
 
@@ -1033,7 +1206,7 @@ int prt_render_multi(void* const* scenes, int n_scenes, const float* cam, int W,
     for (int r = 0; r < n_scenes; ++r) {
         DeviceGuard g(sc[(size_t)r]->device);
         HIP_TRY(hipStreamSynchronize(sc[(size_t)r]->stream));
-        if (read_fault_at(cx[(size_t)r]->work) != 0)
+        if (take_fault_at(cx[(size_t)r]->work) != 0)
             return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped on device " + std::to_string(devs[(size_t)r]));
     }
     return PRT_OK;

@@ -349,13 +349,7 @@ struct SpillStack {
     }
     __device__ __forceinline__ int get(int k) const { return k < LST ? l[k * kBlock] : g[(size_t)(k - LST) * gs]; }
     // wave-uniform: no lane touches an entry above k < LST, so the spill branches can go
-    __device__ __forceinline__ bool lds_only(int k) const {
-#ifdef PRT_AB_NO_LDS_FASTPATH
-        return false;   // A/B: every access takes the spill-aware path
-#else
-        return __ballot(k >= LST) == 0;
-#endif
-    }
+    __device__ __forceinline__ bool lds_only(int k) const { return __ballot(k >= LST) == 0; }
     __device__ __forceinline__ LdsStack lds() const { return LdsStack{l}; }
 };
 // LDS-resident scenes: 16-bit entries (half the stack's LDS, so the octant node copies
@@ -952,9 +946,15 @@ void trace_kernel(TraceParams P) {
                         float4 r = P.rays[item];
                         d = v3(r.x, r.y, r.z);
                         st = __float_as_uint(r.w);
-                        float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
-                        asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
-                        o = v3(o0, o1, o2);
+                        if (P.ray_o) {
+                            // prt_trace_rays: the caller's origin per ray (PathTracer.trace)
+                            const float4 ro = P.ray_o[item];
+                            o = v3(ro.x, ro.y, ro.z);
+                        } else {
+                            float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
+                            asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
+                            o = v3(o0, o1, o2);
+                        }
                     } else {
                         camera_ray(P, x, y, chunk_s, st, o, d);
                     }
@@ -1372,7 +1372,7 @@ void trace_kernel(TraceParams P) {
     X(kVarLds6, 8, true, 6)                   \
     X(kVarGlobalMis, 480, false, 6)
 
-// spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32/64
+// spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
 static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStream_t stream) {
     constexpr bool spill = (VAR & 32) != 0;

@@ -47,7 +47,7 @@ struct Bvh4Host {
     std::vector<float> nodes;      // n_nodes * 32
     int64_t n_nodes = 0;
     int32_t depth = 0;             // max root-to-leaf node count - 1
-    int32_t stack_need = 0;        // worst-case traversal stack entries (3 per level + sentinel)
+    int32_t stack_need = 0;        // worst-case traversal stack entries (collapse_bvh4)
 };
 void collapse_bvh4(const BvhHost& b2, Bvh4Host* out);
 

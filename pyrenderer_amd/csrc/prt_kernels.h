@@ -28,6 +28,7 @@ struct TraceParams {
     int resume_min;           // resume variants: leave the traversal loop below this many active lanes
     int* spill;               // spill variants: per-lane stack entries beyond the LDS part (stride = grid threads)
     const float4* rays;       // primary rays of this launch from camera_kernel, or null (generated in the refill)
+    const float4* ray_o;      // prt_trace_rays: per-item ray origin (rays_kernel), or null (the camera's cam_o)
     float cam_o[3], cam_k[3];
     int W, H;                 // full frame (u = (x + r) / (W - 1))
     float wm1, hm1;           // (float)(W - 1), (float)(H - 1)
@@ -79,6 +80,13 @@ size_t trace_smem_bytes(int stack, int var, const TraceParams& P);
 hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream);
 hipError_t launch_hits(const TraceParams& P, bool quantized, bool any, int stack, const float4* rays, int64_t n,
                        int* hit_id, float* hit_t, hipStream_t stream);
+// World.hit_all's shading at the closest hits of launch_hits (prt_hit_all): n x 16 f32
+hipError_t launch_hit_shade(const TraceParams& P, const float4* rays, int64_t n, const int* hit_id, const float* hit_t,
+                            float* out16, hipStream_t stream);
+// prt_trace_rays: caller rays (n x 8 f32) -> P.rays (d, rng state keyed (seed, i, 0)) and P.ray_o
+// for n_pad >= n items (the padding repeats ray 0)
+hipError_t launch_rays_prep(const TraceParams& P, const float* in8, int64_t n, int64_t n_pad, float4* rays,
+                            float4* ray_o, hipStream_t stream);
 size_t lds_scene_bytes(const TraceParams& P);  // LDS-resident scene + shading data
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);

@@ -22,7 +22,7 @@ namespace prt {
 
 // per-(stack, stats) trace-kernel instantiation sets, compiled in parallel from
 // prt_trace_inst.hip (one object each)
-#define PRT_INST_LIST(X) X(4, 0) X(4, 1) X(10, 0) X(10, 1) X(16, 0) X(16, 1) X(32, 0) X(32, 1) X(64, 0) X(64, 1)
+#define PRT_INST_LIST(X) X(4, 0) X(4, 1) X(10, 0) X(10, 1) X(16, 0) X(16, 1) X(32, 0) X(32, 1)
 #define PRT_DECL_INST(S, T)                                                                              \
     hipError_t launch_trace_##S##_##T(const TraceParams& P, int var, int grid, size_t smem, hipStream_t stream); \
     int trace_occ_##S##_##T(int var, size_t smem);
@@ -97,6 +97,84 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float
     hit_t[i] = hit ? ht : 0.0f;
 }
 
+// World.hit_all's 8-tuple at the closest hits found by hits_kernel (intersection_taichi.py:238-291,
+// Quad.hit / Cube.hit shapes.py:76-110): p = o + t d (ray.at), the face normal flipped toward the
+// ray for two-sided BSDFs, emitting_light, bsdf.evaluate(), and the scatter: a cosine-hemisphere
+// draw (samplers.py:28-32) rotated into rotate_z_to(normal)'s frame (mat4_taichi.py:44-60),
+// pdf = |n.wi| / pi.  The two draws come from the stream keyed (seed, ray index, 0).  Spheres
+// (build-added) take their normal (p - c) / r and build the frame here.
+// out16 per ray: hit, t, p.xyz, n.xyz, emit, rho.rgb, wi.xyz, pdf (zeros after t on a miss).
+__global__ __launch_bounds__(kBlock) void hit_shade_kernel(TraceParams P, const float4* __restrict__ rays, int64_t n,
+                                                           const int* __restrict__ hit_id,
+                                                           const float* __restrict__ hit_t, float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 a = rays[2 * i], b = rays[2 * i + 1];
+    const V3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
+    float r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = 0.0f;
+    const int hid = hit_id[i];
+    r[1] = b.w;   // closest_so_far: t_max on a miss
+    if (hid >= 0) {
+        const float t = hit_t[i];
+        const V3 p = o + d * t;
+        V3 ng;
+        int mid;
+        if (hid < P.n_tri) {
+            const float4 nm = P.tri_nm[hid];
+            ng = xyz(nm);
+            mid = __float_as_int(nm.w);
+        } else {
+            const float4 sc = P.sph[hid - P.n_tri];
+            ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
+            mid = P.sph_mat[hid - P.n_tri];
+        }
+        const float* m = P.mats + 8 * mid;
+        const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;
+        const V3 nn = flip ? neg(ng) : ng;
+        uint32_t st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)i, 0u);
+        const float u0 = rng_next(st);
+        const float u1 = rng_next(st);
+        const V3 l = cosine_hemisphere<false>(u0, u1);
+        V3 wi;
+        if (hid < P.n_tri) {
+            const float4* fr = P.tri_frame + ((size_t)hid * 2 + (flip ? 1 : 0)) * 3;
+            wi = normalize(xyz(fr[0]) * l.x + xyz(fr[1]) * l.y + xyz(fr[2]) * l.z);
+        } else {
+            wi = to_world(nn, l);
+        }
+        const V3 vals[5] = {p, nn, v3(m[0], m[1], m[2]), wi, v3(0, 0, 0)};
+        r[0] = 1.0f;
+        r[1] = t;
+        r[2] = vals[0].x; r[3] = vals[0].y; r[4] = vals[0].z;
+        r[5] = vals[1].x; r[6] = vals[1].y; r[7] = vals[1].z;
+        r[8] = m[3] != 0.0f ? 1.0f : 0.0f;
+        r[9] = vals[2].x; r[10] = vals[2].y; r[11] = vals[2].z;
+        r[12] = vals[3].x; r[13] = vals[3].y; r[14] = vals[3].z;
+        r[15] = fabsf(dot(nn, wi)) * kInvPi;
+    }
+    float4* o4 = reinterpret_cast<float4*>(out + 16 * i);
+    o4[0] = make_float4(r[0], r[1], r[2], r[3]);
+    o4[1] = make_float4(r[4], r[5], r[6], r[7]);
+    o4[2] = make_float4(r[8], r[9], r[10], r[11]);
+    o4[3] = make_float4(r[12], r[13], r[14], r[15]);
+}
+
+// prt_trace_rays: the caller's rays (o.xyz, -, d.xyz, -) as the trace kernel's primary rays —
+// (d, rng state keyed (seed, i, 0)) and the origin (o, 0) per item; items past n repeat ray 0
+// (the padding to whole 64-item chunks; their radiance is not returned).
+__global__ __launch_bounds__(kBlock) void rays_prep_kernel(TraceParams P, const float* __restrict__ in8, int64_t n,
+                                                           int64_t n_pad, float4* __restrict__ rays,
+                                                           float4* __restrict__ ray_o) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n_pad) return;
+    const float* r = in8 + 8 * (i < n ? i : 0);
+    const uint32_t st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)i, 0u);
+    rays[i] = make_float4(r[4], r[5], r[6], __uint_as_float(st));
+    ray_o[i] = make_float4(r[0], r[1], r[2], 0.0f);
+}
+
 // Packed tile slots -> a window [x0, x0+w) x [y0, y0+h) of the frame, indexed [x][y]
 // like the reference's pixels.to_numpy() (main_taichi.py:25): out[((x-x0)*h + (y-y0))*3 + c].
 // tile_xy = (x0 << 16) | y0 per tile (the trace kernel's tile origins); slots outside the
@@ -137,8 +215,9 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
 
 }  // namespace
 
-// entries needed: one per level (<= depth) plus the while-while sentinel
-int stack_variant(int depth) { return depth + 1 <= 10 ? 10 : depth + 1 <= 16 ? 16 : depth + 1 <= 32 ? 32 : 64; }
+// LDS stack entries of the trace kernel for a BVH4 needing need = depth + 1 entries
+// (collapse_bvh4's bound; scenes needing more than 32 take the spill-stack global variant)
+int stack_variant(int depth) { return depth + 1 <= 10 ? 10 : depth + 1 <= 16 ? 16 : 32; }
 
 // LDS-resident scene (prt_device.h trace_kernel): the BVH4 as 8 octant copies of 7 float4 per
 // node (n_node_f4 counts the 8 float4 of a global BVH4 node), triangles, shading data
@@ -161,7 +240,7 @@ hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool
         case 10: return stats ? launch_trace_10_1(P, var, grid, smem, stream) : launch_trace_10_0(P, var, grid, smem, stream);
         case 16: return stats ? launch_trace_16_1(P, var, grid, smem, stream) : launch_trace_16_0(P, var, grid, smem, stream);
         case 32: return stats ? launch_trace_32_1(P, var, grid, smem, stream) : launch_trace_32_0(P, var, grid, smem, stream);
-        default: return stats ? launch_trace_64_1(P, var, grid, smem, stream) : launch_trace_64_0(P, var, grid, smem, stream);
+        default: return hipErrorInvalidValue;
     }
 }
 
@@ -177,6 +256,20 @@ hipError_t launch_hits(const TraceParams& P, bool quantized, bool any, int stack
         if (any) hits_kernel<false, true><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
         else hits_kernel<false, false><<<grid, kBlock, smem, stream>>>(P, rays, n, hit_id, hit_t);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_hit_shade(const TraceParams& P, const float4* rays, int64_t n, const int* hit_id, const float* hit_t,
+                            float* out16, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hit_shade_kernel<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, stream>>>(P, rays, n, hit_id, hit_t, out16);
+    return hipGetLastError();
+}
+
+hipError_t launch_rays_prep(const TraceParams& P, const float* in8, int64_t n, int64_t n_pad, float4* rays,
+                            float4* ray_o, hipStream_t stream) {
+    if (n_pad <= 0) return hipSuccess;
+    rays_prep_kernel<<<(unsigned)((n_pad + kBlock - 1) / kBlock), kBlock, 0, stream>>>(P, in8, n, n_pad, rays, ray_o);
     return hipGetLastError();
 }
 
@@ -242,7 +335,7 @@ int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem) {
         case 10: return stats ? trace_occ_10_1(var, smem) : trace_occ_10_0(var, smem);
         case 16: return stats ? trace_occ_16_1(var, smem) : trace_occ_16_0(var, smem);
         case 32: return stats ? trace_occ_32_1(var, smem) : trace_occ_32_0(var, smem);
-        default: return stats ? trace_occ_64_1(var, smem) : trace_occ_64_0(var, smem);
+        default: return 0;
     }
 }
 

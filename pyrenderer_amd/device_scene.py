@@ -68,6 +68,21 @@ def unpack_tiles(slots, W, H, tw, th, tile_ids, frame=None):
     return frame
 
 
+def pack_rays(o, d, tmin, tmax):
+    """(n, 8) float32 ray records (o.xyz, t_min, d.xyz, t_max) of the hit / trace entry points."""
+    o = np.asarray(o, np.float32).reshape(-1, 3)
+    d = np.asarray(d, np.float32).reshape(-1, 3)
+    n = o.shape[0]
+    if d.shape[0] != n:
+        raise ValueError(f"{n} ray origins but {d.shape[0]} directions")
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = o
+    rays[:, 3] = np.broadcast_to(np.asarray(tmin, np.float32), (n,))
+    rays[:, 4:7] = d
+    rays[:, 7] = np.broadcast_to(np.asarray(tmax, np.float32), (n,))
+    return rays
+
+
 class DeviceScene:
     def __init__(self, flat, device=0):
         self.flat = flat
@@ -134,21 +149,38 @@ class DeviceScene:
                                                 spp, depth, int(seed), flags, ctypes.c_void_p(d_out_ptr),
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def scatter_tiles(self, d_packed_ptr, tile_ids, tw, th, W, H, d_frame_ptr, stream_ptr=None):
+        """prt_scatter_tiles: packed tile sums (device) -> the device frame (W, H, 3) [x][y], enqueued."""
+        tile_ids = np.ascontiguousarray(tile_ids, np.int32)
+        N.check(N.lib().prt_scatter_tiles(self.h, ctypes.c_void_p(d_packed_ptr), N.ptr(tile_ids), tile_ids.shape[0],
+                                          tw, th, W, H, ctypes.c_void_p(d_frame_ptr),
+                                          ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
     def closest_hits(self, o, d, tmin, tmax, any_hit=False, quantized=False):
         """World.hit_all on the GPU for arrays of rays: (hit_id, t); id -1 = miss."""
-        o = np.asarray(o, np.float32).reshape(-1, 3)
-        d = np.asarray(d, np.float32).reshape(-1, 3)
-        n = o.shape[0]
-        rays = np.zeros((n, 8), np.float32)
-        rays[:, 0:3] = o
-        rays[:, 3] = np.broadcast_to(np.asarray(tmin, np.float32), (n,))
-        rays[:, 4:7] = d
-        rays[:, 7] = np.broadcast_to(np.asarray(tmax, np.float32), (n,))
+        rays = pack_rays(o, d, tmin, tmax)
+        n = rays.shape[0]
         hid = np.zeros(n, np.int32)
         ht = np.zeros(n, np.float32)
         flags = (N.PRT_HITS_ANY if any_hit else 0) | (N.PRT_HITS_QUANTIZED if quantized else 0)
         N.check(N.lib().prt_closest_hits(self.h, N.ptr(rays), n, flags, N.ptr(hid), N.ptr(ht)))
         return hid, ht
+
+    def hit_all(self, o, d, tmin, tmax, seed=0, quantized=False):
+        """prt_hit_all: World.hit_all's 8-tuple per ray as (n, 16) float32 rows — hit, t, p.xyz,
+        normal.xyz, emit, attenuation.rgb, scattered direction.xyz, pdf (include/prt.h)."""
+        rays = pack_rays(o, d, tmin, tmax)
+        out = np.zeros((rays.shape[0], 16), np.float32)
+        N.check(N.lib().prt_hit_all(self.h, N.ptr(rays), rays.shape[0], int(seed),
+                                    N.PRT_HITS_QUANTIZED if quantized else 0, N.ptr(out)))
+        return out
+
+    def trace_rays(self, o, d, depth, seed=0, flags=0):
+        """prt_trace_rays: PathTracer.trace's radiance for each caller ray, (n, 3) float32."""
+        rays = pack_rays(o, d, 0.0, 0.0)
+        out = np.zeros((rays.shape[0], 3), np.float32)
+        N.check(N.lib().prt_trace_rays(self.h, N.ptr(rays), rays.shape[0], int(depth), int(seed), flags, N.ptr(out)))
+        return out
 
     def kernel_info(self):
         """Default trace-kernel variant: dict(variant, bvh_arity, lds_scene, quantized, stack)."""

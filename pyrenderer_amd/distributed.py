@@ -44,15 +44,35 @@ class TileShard:
                 self.wire.copy_(self.buf)       # synchronous device-to-host copy on the current stream
             dist.gather(self.wire, self.gather_list, dst=0, group=group)
 
-    def assemble(self):
-        """Rank 0: (W, H, 3) float32 sums frame from the gathered buffers."""
-        frame = np.zeros((self.W, self.H, 3), np.float32)
+    def assemble(self, device_scene=None, stream=None):
+        """Rank 0: (W, H, 3) float32 sums frame from the gathered buffers.
+
+        With `device_scene` (GPU ranks) the tiles are scattered into a device frame by libprt's
+        scatter kernel (prt_scatter_tiles) on `stream` (default: torch's current stream) — the
+        gathered buffers, already on the device over RCCL or uploaded once from gloo's host
+        staging, never pass through a host loop; the frame is then copied to the host.  Without
+        it (CPU-tensor shards: the gloo tests with the CPU oracle as renderer) the tiles are
+        unpacked in numpy."""
         bufs = self.gather_list if self.world > 1 else [self.buf]
-        for r, b in enumerate(bufs):
-            ids = interleaved_tiles(self.W, self.H, self.tile, r, self.world, self.scheme)
-            n = len(ids) * self.slot_elems
-            unpack_tiles(b[:n].cpu().numpy().reshape(-1, 3), self.W, self.H, self.tile, self.tile, ids, frame)
-        return frame
+        per_rank = [interleaved_tiles(self.W, self.H, self.tile, r, self.world, self.scheme) for r in range(self.world)]
+        if device_scene is None:
+            frame = np.zeros((self.W, self.H, 3), np.float32)
+            for b, ids in zip(bufs, per_rank):
+                n = len(ids) * self.slot_elems
+                unpack_tiles(b[:n].cpu().numpy().reshape(-1, 3), self.W, self.H, self.tile, self.tile, ids, frame)
+            return frame
+        dev = torch.device("cuda", device_scene.device)
+        s = stream or torch.cuda.current_stream(dev)
+        with torch.cuda.stream(s):
+            packed = torch.cat([b[:len(ids) * self.slot_elems].to(dev, non_blocking=False)
+                                for b, ids in zip(bufs, per_rank)])
+            frame = torch.zeros((self.W, self.H, 3), dtype=torch.float32, device=dev)
+        ids = np.concatenate(per_rank).astype(np.int32)
+        device_scene.scatter_tiles(packed.data_ptr(), ids, self.tile, self.tile, self.W, self.H, frame.data_ptr(),
+                                   s.cuda_stream)
+        with torch.cuda.stream(s):
+            out = frame.cpu().numpy()
+        return out
 
 
 def render_distributed(device_scene, cam_packed, W, H, spp, depth, seed=0, tile=64, group=None, stream=None):
@@ -91,5 +111,4 @@ def render_distributed(device_scene, cam_packed, W, H, spp, depth, seed=0, tile=
         shard.gather(group)
     if rank != 0:
         return None
-    torch.cuda.synchronize(dev)
-    return shard.assemble() / np.float32(max(spp, 1))
+    return shard.assemble(device_scene, s) / np.float32(max(spp, 1))

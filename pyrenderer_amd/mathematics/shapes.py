@@ -11,6 +11,7 @@ winding is reversed when det(M[:3,:3]) < 0.  Normals: Quad uses
 computed in float64 and stored float32 as the reference's arrays are.
 """
 import math
+import random
 
 import numpy as np
 
@@ -68,6 +69,19 @@ class _MeshPrimitive:
     @property
     def bounding_box(self):
         return self.bounds.min_coord, self.bounds.max_coord
+
+    def sample_a_point(self, rng=random):
+        """A uniform point on a random face (the reference's NumPy twin, shapes2.py:72-79, used by
+        Scene.sample_light): face randint(0, F-1), u = sqrt(U), v = U, a = u(1-v), b = uv,
+        a V0 + b V1 + (1-a-b) V2.  Host-side (debug API); the kernel's light sampling is
+        World.sample_a_light's (shapes.py:62-71) on the GPU."""
+        face_id = rng.randint(0, self.faces.shape[0] - 1)
+        u = math.sqrt(rng.uniform(0, 1))
+        v = rng.uniform(0, 1)
+        a = u * (1 - v)
+        b = u * v
+        v0, v1, v2 = self.faces[face_id]
+        return a * self.vertices[v0] + b * self.vertices[v1] + (1.0 - a - b) * self.vertices[v2]
 
 
 class Quad(_MeshPrimitive):

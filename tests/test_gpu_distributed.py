@@ -107,3 +107,40 @@ def test_watchdog_is_reported_on_every_path(cornell, monkeypatch):
     ok.check_faults()
     assert render_distributed(ok, cam, 64, 64, 4, 8).sum() > 0
     ok.close()
+
+
+def test_watchdog_flags_are_reported_once(cornell, monkeypatch):
+    """a fault is reported by the call that checks the launch that raised it, then
+    cleared — a device-output render on a fresh scene reports its own fault, and a clean
+    device-output render after a faulted one (on another stream, or after a faulted hit query)
+    is not blamed for it."""
+    import torch
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    ids = np.arange(4, dtype=np.int32)
+    buf = torch.empty(4 * 32 * 32 * 3, dtype=torch.float32, device="cuda:0")
+    monkeypatch.setenv("PRT_GUARD_TRIPS", "1")
+    ds = DeviceScene(cornell[2], 0)
+    side = torch.cuda.Stream(torch.device("cuda", 0))
+    # only a device-output render on the fresh scene: its fault is reported
+    ds.render_tiles_device(cam, 64, 64, 32, 32, ids, 4, 8, buf.data_ptr(), side.cuda_stream)
+    with pytest.raises(N.PrtError) as e:
+        ds.check_faults()
+    assert e.value.code == N.PRT_ERR_INTERNAL
+    ds.check_faults()                     # reported once: nothing new since
+    # a faulted render on one stream, then a clean (no-work) render on another
+    ds.render_tiles_device(cam, 64, 64, 32, 32, ids, 4, 8, buf.data_ptr(), side.cuda_stream)
+    with pytest.raises(N.PrtError):
+        ds.check_faults()
+    ds.render_tiles_device(cam, 64, 64, 32, 32, ids, 0, 8, buf.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    ds.check_faults()
+    # a faulted hit query (reported by the query itself), then a clean device-output render
+    rng = np.random.default_rng(0)
+    o = rng.uniform((-0.9, 0.1, -0.9), (0.9, 1.9, 0.9), (4096, 3)).astype(np.float32)
+    d = rng.normal(size=(4096, 3)).astype(np.float32)
+    with pytest.raises(N.PrtError, match="watchdog"):
+        ds.closest_hits(o, d, 1e-5, 99999.9)
+    ds.render_tiles_device(cam, 64, 64, 32, 32, ids, 0, 8, buf.data_ptr(), side.cuda_stream)
+    ds.check_faults()
+    ds.close()

@@ -37,6 +37,44 @@ def test_hit_all_bit_exact(oracle_scene, cornell, backend):
     np.testing.assert_array_equal(cornell[2].mat[cornell[2].tri_mat[tri[m]], :3], h["rho"][m])
 
 
+def test_hit_all_tuple_matches_reference(oracle_scene):
+    """The batch World.hit_all 8-tuple (or_hit_all_batch, the checker of prt_hit_all): hit, t,
+    normal, emissive and attenuation equal the reference's on the 3009 golden queries; misses
+    keep closest_so_far; the scatter is a unit direction above the normal with pdf |n.wi|/pi."""
+    h = golden("hits_cornell.npz")
+    out = oracle_scene.hit_all(h["ro"], h["rd"], h["tmin"], h["tmax"], seed=5)
+    m = h["hit"] != 0
+    np.testing.assert_array_equal(out[:, 0] > 0, m)
+    np.testing.assert_array_equal(out[m, 1], h["t"][m])
+    np.testing.assert_array_equal(out[~m, 1], h["tmax"][~m])
+    np.testing.assert_array_equal(out[m, 5:8], h["normal"][m])
+    np.testing.assert_array_equal(out[m, 8], h["emit"][m].astype(np.float32))
+    np.testing.assert_array_equal(out[m, 9:12], h["rho"][m])
+    wi, n, pdf = out[m, 12:15], out[m, 5:8], out[m, 15]
+    np.testing.assert_allclose(np.linalg.norm(wi, axis=1), 1.0, atol=1e-6)
+    cos = np.einsum("ij,ij->i", wi, n)
+    assert (cos >= -1e-6).all()
+    np.testing.assert_allclose(pdf, np.abs(cos) / np.pi, rtol=1e-5, atol=1e-7)
+    assert not out[~m][:, [0] + list(range(2, 16))].any()
+
+
+def test_trace_rays_backends_agree(oracle_scene, cornell):
+    """PathTracer.trace for caller rays (or_trace_rays, the checker of prt_trace_rays): the
+    reference-structure, brute-force and BVH2 backends give identical radiance."""
+    from pyrenderer_amd._native import Bvh
+    rng = np.random.default_rng(2)
+    o = rng.uniform((-0.9, 0.1, -0.9), (0.9, 1.9, 0.9), (600, 3)).astype(np.float32)
+    d = rng.normal(size=(600, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    nodes, _, order = Bvh(cornell[2].tri_v).export()
+    osc = O.OracleScene.from_flat(cornell[2])
+    osc.set_bvh(nodes, order)
+    ref = osc.trace_rays(o, d, 8, seed=3, backend=O.BACKEND_REF)
+    assert ref.mean() > 0
+    np.testing.assert_array_equal(ref, osc.trace_rays(o, d, 8, seed=3, backend=O.BACKEND_BRUTE))
+    np.testing.assert_array_equal(ref, osc.trace_rays(o, d, 8, seed=3, backend=O.BACKEND_BVH))
+
+
 def test_test_py_recorded_bounces(oracle_scene):
     """test.py:38-57: t to the 6 printed digits, normal and albedo of all 9 segments."""
     h = golden("hits_cornell.npz")
