@@ -24,8 +24,10 @@ VAR_LDS_ANY_OCC = 2   # ... without the occupancy target
 VAR_GLOBAL = 3        # scene in HBM: quantised BVH4, LDS stack + global spill, suspended tails
 VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
 VAR_LDS6 = 6          # VAR_LDS built for >= 6 waves/SIMD (LDS copies that fit 6 but not 7 blocks per CU)
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6)
-VAR_LAST = 6
+VAR_LDS_POOL = 7      # LDS-resident scene, block-pooled shadow queries (trace_kernel_pool)
+VAR_LDS_POOL6 = 8     # VAR_LDS_POOL built for >= 6 waves/SIMD
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6)
+VAR_LAST = 8
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 

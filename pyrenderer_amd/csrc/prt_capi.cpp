@@ -267,16 +267,23 @@ bool lds_fits4(const Scene* s) {
 // Everything else (and BVH4s deeper than the 64-entry LDS stack) takes the global-scene
 // kernel: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal tails,
 // >= 6 waves/SIMD (C4: 28.6 ms at 5 waves, 27.2 at 6, 28.6 at 7 with spills).
+// An LDS-resident scene whose pooled-shadow kernel still fits seven blocks per CU takes that kernel
+// (C2 4.13 vs 4.28 ms, C3 at 32 spp 9.70 vs 10.10 ms, profiles/r03/s7/).
 int default_variant(const Scene* s) {
     if (!lds_fits4(s) || !s->stack4) return prt::kVarGlobal;
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
     scene_sizes(s, P);
+    P.lds_stack = s->need4;
+    if (s->need4 <= 32 && prt::trace_smem_bytes(16, prt::kVarLdsPool, P) * 7 <= 160 * 1024) return prt::kVarLdsPool;
     size_t smem = prt::trace_smem_bytes(s->stack4, prt::kVarLds, P);
     return smem * 7 <= 160 * 1024 ? prt::kVarLds : smem * 6 <= 160 * 1024 ? prt::kVarLds6 : prt::kVarLdsAnyOcc;
 }
-// the traversal stack entries of variant `var` (LDS part for the spill variants)
-int variant_stack(const Scene* s, int var) { return prt::variant_spills(var) ? s->spill_lds : s->stack4; }
+// the traversal stack entries of variant `var` (LDS part for the spill variants; the pool kernel's
+// instantiation set, its LDS stack being the launch parameter P.lds_stack)
+int variant_stack(const Scene* s, int var) {
+    return prt::variant_pool(var) ? 16 : prt::variant_spills(var) ? s->spill_lds : s->stack4;
+}
 
 // Pinhole camera with an affine matrix (no aperture, last row (0,0,0,1), all finite):
 // the kernels may use the exact gen_ray shortcut (TraceParams::cam_fast).
@@ -327,6 +334,8 @@ int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, prt::TraceParams& P, in
         P.n_node_f4 = (int)s->n_node4q_f4;
     }
     if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
+    if (prt::variant_pool(var) && (s->need4 > 32 || s->need4 < 1))
+        return fail(PRT_ERR_ARG, "BVH4 too deep for the pooled-shadow variant's LDS stack");
     // while-while leaf-phase entry: LDS scenes wait for every descending lane's leaf (their
     // leaves are cheap and traversals short); global scenes enter the leaf phase once at
     // most 16 descending lanes still lack one (C4: 35.1 -> 29.7 ms at 8 in round 1, 18.69 ->
@@ -336,6 +345,7 @@ int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, prt::TraceParams& P, in
     // chunks 17.37-17.46 ms at 24 against 17.50-17.64 at 12 in three interleaved rounds,
     // profiles/r03/s1_baseline/leafexit/)
     const bool lds_var = prt::variant_uses_lds(var);
+    P.lds_stack = s->need4;
     P.leaf_break = s->leaf_break >= 0 ? s->leaf_break : (lds_var ? 0 : 16);
     P.leaf_exit = s->leaf_exit >= 0 ? s->leaf_exit : (lds_var ? 8 : 24);
     int& occ = s->occ[2 * var + (stats ? 1 : 0)];
@@ -734,6 +744,7 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             std::memset(&Q, 0, sizeof(Q));
             int var = default_variant(s);
             scene_sizes(s, Q);
+            Q.lds_stack = s->need4;
             int stk = variant_stack(s, var);
             s->blocks_per_cu = std::max(1, prt::trace_blocks_per_cu(stk, var, false, prt::trace_smem_bytes(stk, var, Q)));
         }

@@ -1361,22 +1361,504 @@ void trace_kernel(TraceParams P) {
     }
 }
 
+// Block copy of an LDS-resident scene's BVH4 as 8 octant copies per node (visit_node4 OCT): copy
+// k of node n holds the near / far planes of each axis for the direction signs k = sx | sy << 1 |
+// sz << 2, then the refs with the empty-slot reference rewritten to the 16-bit stack's sentinel,
+// the four children in k's front-to-back order (ascending near corner along the octant's
+// diagonal, empty slots last, ties by index).  The same layout as trace_kernel's copy loop.
+__device__ __forceinline__ void copy_octant_nodes(float4* __restrict__ sn, const float4* __restrict__ nodes,
+                                                  int n_node4) {
+    for (int i = threadIdx.x; i < 56 * n_node4; i += kBlock) {
+        const int n = i / 56, r = i - 56 * n, k = r / 7, slot = r - 7 * k;
+        const int ax = slot >> 1, sgn = (k >> ax) & 1, far = slot & 1;
+        const float4* src = nodes + 8 * n;
+        float4 v = slot == 6 ? src[6] : src[2 * ax + (sgn ^ far)];
+        if (slot == 6) {
+            int* rr = reinterpret_cast<int*>(&v);
+            for (int c = 0; c < 4; ++c) rr[c] = rr[c] == kSentinel ? LdsStack16::kSent : rr[c];
+        }
+        float key[4];
+        {
+            const float4 lx = src[0], hx = src[1], ly = src[2], hy = src[3], lz = src[4], hz = src[5];
+            const float4 rf = src[6];
+            const int rr[4] = {__float_as_int(rf.x), __float_as_int(rf.y), __float_as_int(rf.z), __float_as_int(rf.w)};
+            const float nxv[4] = {lx.x, lx.y, lx.z, lx.w}, fxv[4] = {hx.x, hx.y, hx.z, hx.w};
+            const float nyv[4] = {ly.x, ly.y, ly.z, ly.w}, fyv[4] = {hy.x, hy.y, hy.z, hy.w};
+            const float nzv[4] = {lz.x, lz.y, lz.z, lz.w}, fzv[4] = {hz.x, hz.y, hz.z, hz.w};
+            for (int c = 0; c < 4; ++c) {
+                key[c] = rr[c] == kSentinel ? INFINITY
+                                            : ((k & 1) ? -fxv[c] : nxv[c]) + ((k & 2) ? -fyv[c] : nyv[c]) +
+                                                  ((k & 4) ? -fzv[c] : nzv[c]);
+                if (!(key[c] == key[c])) key[c] = INFINITY;
+            }
+        }
+        const float vin[4] = {v.x, v.y, v.z, v.w};
+        int rank[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            rank[c] = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rank[c] += (key[e] < key[c] || (key[e] == key[c] && e < c)) ? 1 : 0;
+        }
+        float vout[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            vout[j] = rank[0] == j ? vin[0] : rank[1] == j ? vin[1] : rank[2] == j ? vin[2] : vin[3];
+        sn[i] = make_float4(vout[0], vout[1], vout[2], vout[3]);
+    }
+}
+
+// Block-pooled shadow queries (LDS-resident scenes, the reference estimator).
+//
+// trace_kernel's phase-aligned waves alternate an extension iteration (62.5 of 64 lanes query at
+// config 2) with a shadow iteration in which only the ~38 lanes that drew an NEE ray query, and
+// those shadow iterations took 43 % of the wave time.  Here the four waves of a block run in
+// lockstep phases instead:
+//   E: every wave refills its idle lanes and runs one closest-hit extension query per busy lane,
+//      then shades it; a lane whose NEE sample needs a visibility test writes the shadow ray
+//      (o = p, d = w, t_max = t_at_light) to its slot of the block's LDS pool and its thread id
+//      to the block's shadow queue;
+//   S: (after a barrier) the queue's n rays are traversed by the first ceil(n / 64) waves, 64
+//      per wave — whichever wave issued them — and each lane writes the any-hit result to the
+//      owner's slot; the other waves are idle (their SIMD slots go to other blocks' waves);
+//   R: (after a second barrier) each owner adds its pending NEE radiance if unoccluded and moves
+//      on to its next bounce.
+// So shadow rays are traversed 64 to a wave instead of ~38, and a lane waits for its shadow
+// result without blocking its wave's next extension query.  Before writing a shadow ray, the
+// lane tests it against the sampled light triangle itself (one exact Moller-Trumbore test in
+// the traversal's arithmetic): the reference's t_at_light bound lets the light occlude itself
+// (SURVEY.md §0), and such a ray is answered without a query.  The result of every query is
+// unchanged (an any-hit query answers "hit" iff some triangle passes the test, whichever is
+// tested first), so images stay bit-identical to trace_kernel's and to the oracle's.
+//
+// LDS (per 256-thread block): the 16-bit traversal stacks (P.lds_stack entries), the pool (7
+// f32 arrays of 256: o.xyz, d.xyz, t_max; t_max carries the result back), the queue (256 u8),
+// two parity-alternating control words pairs (queue length, "alive"), then the scene copy:
+// octant BVH4 nodes, triangles, light triangles and offsets.  Shading data (normals, frames,
+// materials) are read from global memory (L1-resident) to keep seven blocks per CU.
+constexpr int kPoolF4 = 7 * kBlock / 4;        // pool SoA: 7 x 256 f32
+constexpr int kQueueF4 = kBlock / 16;          // queue: 256 u8
+constexpr int kCtlF4 = 2;                      // ctl: count[2], alive[2], chunk claims[2]
+#ifndef PRT_POOL_S_PRIO
+#define PRT_POOL_S_PRIO 2
+#endif
+
+template <bool STATS, int WPE>
+__global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
+void trace_kernel_pool(TraceParams P) {
+    extern __shared__ float4 smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int stack_f4 = P.lds_stack * kBlock * 2 / 16;
+    LdsStack16 stk;
+    stk.l = reinterpret_cast<short*>(smem) + (tid & ~63) + 2 * (tid & 31) + ((tid >> 5) & 1);
+    float* pool = reinterpret_cast<float*>(smem + stack_f4);   // [7][256]
+    uint8_t* queue = reinterpret_cast<uint8_t*>(smem + stack_f4 + kPoolF4);
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + stack_f4 + kPoolF4 + kQueueF4);
+    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + kCtlF4;
+    const int n_node4 = P.n_node_f4 / 8;
+    float4* st4 = sn + 56 * n_node4;
+    float4* slv = st4 + P.n_tri_f4;
+    int* slo = reinterpret_cast<int*>(slv + 4 * P.n_lt);
+    copy_octant_nodes(sn, P.nodes, n_node4);
+    for (int i = tid; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
+    for (int i = tid; i < 4 * P.n_lt; i += kBlock) slv[i] = P.light_v[i];
+    for (int i = tid; i <= P.n_light; i += kBlock) slo[i] = P.light_off[i];
+    if (tid < 6) ctl[tid] = 0u;
+    __syncthreads();
+    const float4* g_nodes = sn;
+    const float4* g_tris = st4;
+    const float4* s_nm = P.tri_nm;
+    const float4* s_fr = P.tri_frame;
+    const float* s_mats = P.mats;
+
+    uint32_t q_next = 0, q_end = 0;
+    bool exhausted = false;
+    int item = -1;
+    int bounce = 0;
+    bool my_sh = false;      // this lane waits for the result of its pooled shadow ray
+    uint32_t st = 0;
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
+    V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t n_e = 0, n_s = 0, lanes_s = 0, pre_hits = 0;
+    uint32_t chunk_s = 0, chunk_xy0 = 0;
+    int parity = 0;
+#ifdef PRT_POOL_CLOCKS
+    // diagnostic build (tools/pool_clocks.py): wave-level cycles in E, at barrier 1, in S, at barrier 2
+    uint64_t ck[4] = {0, 0, 0, 0};
+    uint64_t t_c = __builtin_amdgcn_s_memtime();
+#define PRT_CLOCK(k) do { const uint64_t t_n = __builtin_amdgcn_s_memtime(); ck[k] += t_n - t_c; t_c = t_n; } while (0)
+#else
+#define PRT_CLOCK(k) do {} while (0)
+#endif
+    // work-queue refill of the wave's idle lanes (path regeneration, trace_kernel's refill)
+    auto refill = [&]() {
+            bool me_idle = item < 0;
+            uint64_t idle = __ballot(me_idle);
+            for (int round = 0; round < 2 && idle; ++round) {
+                uint32_t avail = q_end - q_next;
+                if (avail == 0 && !exhausted) {
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(P.work, (uint32_t)kChunk);
+                    base = __builtin_amdgcn_readfirstlane(base);
+                    if ((uint64_t)base >= P.n_items) {
+                        exhausted = true;
+                    } else {
+                        q_next = base;
+                        q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
+                        chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
+                        uint32_t tk = (base - chunk_s * (uint32_t)P.n_slots) >> P.log_tpx;
+                        chunk_xy0 = ((const __attribute__((address_space(4))) uint32_t*)(uintptr_t)P.tile_xy)[tk];
+                    }
+                    avail = q_end - q_next;
+                }
+                if (avail == 0) break;
+                uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                uint32_t need = (uint32_t)__popcll(idle);
+                uint32_t take = need < avail ? need : avail;
+                if (me_idle && rank < take) {
+                    item = (int)(q_next + rank);
+                    L = v3(0, 0, 0);
+                    int x, y;
+                    pixel_of(P, (uint32_t)item, chunk_s, chunk_xy0, x, y);
+                    int W = P.W, H = P.H;
+                    asm volatile("" : "+s"(W), "+s"(H));
+                    bool ok = x < W && y < H;
+                    if (ok) {
+                        if (P.rays) {
+                            float4 r = P.rays[item];
+                            d = v3(r.x, r.y, r.z);
+                            st = __float_as_uint(r.w);
+                            if (P.ray_o) {
+                                const float4 ro = P.ray_o[item];
+                                o = v3(ro.x, ro.y, ro.z);
+                            } else {
+                                float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
+                                asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
+                                o = v3(o0, o1, o2);
+                            }
+                        } else {
+                            camera_ray(P, x, y, chunk_s, st, o, d);
+                        }
+                    }
+                    if (!ok) {
+                        float* out = P.out + (size_t)item * 3;
+                        out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
+                        item = -2;
+                    } else {
+                        beta = v3(1, 1, 1);
+                        bounce = 0;
+                        // the primary ray as this lane's next ray (R takes o from the pool, d from wi)
+                        pool[0 * kBlock + tid] = o.x; pool[1 * kBlock + tid] = o.y; pool[2 * kBlock + tid] = o.z;
+                        wi = d;
+                    }
+                }
+                q_next += take;
+                me_idle = item == -1;
+                idle = __ballot(me_idle);
+            }
+        if (item == -2) item = -1;
+    };
+    while (true) {
+        // ------------------------------------------------------------------ E phase
+        refill();
+        if (__ballot(item >= 0) != 0) {
+            if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_e++;
+            if (item >= 0) {
+                int hid = -1;
+                float ht = 0.0f;
+                if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
+                bool hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
+                    g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
+                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
+                if (P.n_sph > 0) {
+                    float best = hit ? ht : kTMax;
+                    for (int k = 0; k < P.n_sph; ++k) {
+                        float root;
+                        if (sphere_hit(P.sph[k], o, d, kTMin, best, root)) {
+                            best = root;
+                            hid = P.n_tri + k;
+                            hit = true;
+                        }
+                    }
+                    ht = best;
+                }
+                bool finished = false;
+                if (!hit) {
+                    finished = true;
+                } else {
+                    V3 p = o + d * ht;
+                    V3 ng;
+                    int mid;
+                    if (hid < P.n_tri) {
+                        float4 nm = s_nm[hid];
+                        ng = xyz(nm);
+                        mid = __float_as_int(nm.w);
+                    } else {
+                        asm volatile("");
+                        float4 sc = P.sph[hid - P.n_tri];
+                        ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
+                        mid = P.sph_mat[hid - P.n_tri];
+                    }
+                    const float* m = s_mats + 8 * mid;
+                    const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;
+                    const V3 n = flip ? neg(ng) : ng;
+                    if (m[5] == 2.0f || m[5] == 3.0f) {
+                        bool front = dot(d, ng) < 0.0f;
+                        V3 ns = front ? ng : neg(ng);
+                        V3 unit = normalize(d);
+                        V3 out;
+                        bool absorbed = false;
+                        if (m[5] == 2.0f) {
+                            out = reflect3(unit, ns);
+                            if (m[7] > 0.0f) out = out + random_in_unit_sphere(st) * m[7];
+                            absorbed = !(dot(out, ns) > 0.0f);
+                        } else {
+                            float ratio = front ? 1.0f / m[6] : m[6];
+                            float ct = -dot(unit, ns);
+                            ct = ct > 1.0f ? 1.0f : ct;
+                            float stn = sqrtf(1.0f - ct * ct);
+                            bool cannot = ratio * stn > 1.0f;
+                            if (cannot || schlick(ct, ratio) > rng_next(st)) out = reflect3(unit, ns);
+                            else out = refract3(unit, ns, ratio);
+                        }
+                        if (absorbed) {
+                            finished = true;
+                        } else {
+                            beta = beta * v3(m[0], m[1], m[2]);
+                            wi = normalize(out);   // next ray (p, wi), taken up in R
+                            ++bounce;
+                            if (bounce >= P.depth) finished = true;
+                        }
+                    } else if (m[3] != 0.0f) {
+                        float d1 = dot(neg(d), n);
+                        if (d1 > 0.0f) {
+                            V3 lc = v3(P.dl_r, P.dl_g, P.dl_b);
+                            L = bounce == 0 ? L + lc * beta : L + (lc * beta) * d1;
+                        }
+                        finished = true;
+                    } else {
+                        float u0 = rng_next(st);
+                        float u1 = rng_next(st);
+                        V3 l = cosine_hemisphere<true>(u0, u1);
+                        const float4* fr = s_fr + ((size_t)(hid < P.n_tri ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
+                        if (hid < P.n_tri) {
+                            float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
+                            wi = normalize<true>(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
+                        } else {
+                            wi = to_world(n, l);
+                        }
+                        float pdf = fabsf(dot(n, wi)) * kInvPi;
+                        V3 att = v3(m[0], m[1], m[2]);
+                        float cw = dot(n, wi);
+                        float dz = cw > 0.0f ? cw : 0.0f;
+                        V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
+                        V3 adp = div3_nan_guard(ad, pdf);
+                        V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
+                        beta = beta * nb;
+                        int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
+                        int lo = slo[li];
+                        int f = rng_int(st, 0, slo[li + 1] - lo - 1);
+                        float su = sqrt_cr<true>(rng_next(st));
+                        float sv = rng_next(st);
+                        float a = su * (1.0f - sv);
+                        float b = su * sv;
+                        const float4* lv = slv + (size_t)(lo + f) * 4;
+                        float4 L0 = lv[0], L1 = lv[1], L2 = lv[2], LN = lv[3];
+                        float c = 1.0f - a - b;
+                        V3 p2 = (xyz(L0) * a + xyz(L1) * b) + xyz(L2) * c;
+                        V3 n2 = xyz(LN);
+                        V3 w = normalize<true>(p2 - p);
+                        float t_at = (p2.x - p.x) / w.x;
+                        float dot1 = dot(n, w), dot2 = -dot(n2, w);
+                        bool queued = false;
+                        if (dot1 > 0.0f && dot2 > 0.0f) {
+                            if (STATS) cn.shadow++;
+                            // the sampled light triangle itself, in the traversal's arithmetic: a hit
+                            // in (t_min, t_at_light) answers the any-hit query (occluded)
+                            float tl;
+                            const V3 lv0 = xyz(L0);
+                            const bool self_hit = mt_u(lv0, xyz(L1) - lv0, xyz(L2) - lv0, p, w, kTMin, t_at, 0, -1,
+                                                       true, tl);
+                            if (STATS) { cn.tris++; pre_hits += self_hit ? 1 : 0; }
+                            if (!self_hit) {
+                                const float* em = s_mats + 8 * __float_as_int(LN.w);
+                                V3 dd = p - p2;
+                                float sl = dot(dd, dd);
+                                V3 rad = div3(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl);
+                                pend = beta * rad;
+                                pool[3 * kBlock + tid] = w.x; pool[4 * kBlock + tid] = w.y; pool[5 * kBlock + tid] = w.z;
+                                pool[6 * kBlock + tid] = t_at;
+                                queued = true;
+                            }
+                        }
+                        if (queued) {
+                            my_sh = true;
+                        } else {
+                            ++bounce;
+                            if (bounce >= P.depth) finished = true;
+                        }
+                    }
+                    // every continuing lane parks its next ray's origin p in its pool slot (the
+                    // shadow ray's origin too) and its direction in wi: neither stays live in
+                    // registers across the S phase, where the lane may traverse another lane's ray
+                    pool[0 * kBlock + tid] = p.x; pool[1 * kBlock + tid] = p.y; pool[2 * kBlock + tid] = p.z;
+                }
+                if (finished) {
+                    float* out = P.out + (size_t)item * 3;
+                    out[0] = L.x; out[1] = L.y; out[2] = L.z;
+                    if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
+                    item = -1;
+                }
+            }
+        }
+        // enqueue this wave's shadow rays: one LDS atomic per wave, thread ids at the ranks
+        {
+            const uint64_t m = __ballot(my_sh);
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            uint32_t base = 0;
+            if (cnt) {
+                if (lane == __builtin_amdgcn_readfirstlane(lane)) base = atomicAdd(&ctl[parity], cnt);
+                base = __builtin_amdgcn_readfirstlane(base);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (my_sh) queue[base + rank] = (uint8_t)tid;
+            }
+            // a wave with busy lanes or unclaimed work keeps the block looping
+            if ((__ballot(item >= 0) != 0 || !exhausted) && lane == 0) ctl[2 + parity] = 1u;
+        }
+        PRT_CLOCK(0);
+        __syncthreads();
+        PRT_CLOCK(1);
+        // ------------------------------------------------------------------ S phase
+        const uint32_t n_q = ctl[parity];
+        if (tid == 0) { ctl[parity ^ 1] = 0u; ctl[2 + (parity ^ 1)] = 0u; ctl[4 + (parity ^ 1)] = 0u; }
+        // the queue's 64-ray chunks go to the first waves to claim one (<= 4 chunks, one claim per
+        // wave); the others refill the lanes that finished in E meanwhile, off the critical path
+        const uint32_t n_chunks = (n_q + 63u) >> 6;
+        uint32_t chunk = 0xFFFFFFFFu;
+        if (n_chunks) {
+            if (lane == 0) chunk = atomicAdd(&ctl[4 + parity], 1u);
+            chunk = __builtin_amdgcn_readfirstlane(chunk);
+        }
+        if (chunk >= n_chunks) refill();
+        if (chunk < n_chunks) {
+            // the S waves hold up their whole block at barrier 2: issue priority over other blocks
+            __builtin_amdgcn_s_setprio(PRT_POOL_S_PRIO);
+            const uint32_t e = chunk * 64u + (uint32_t)lane;
+            if (STATS && lane == 0) { n_s++; lanes_s += min(n_q - chunk * 64u, 64u); }
+            if (e < n_q) {
+                const int owner = queue[e];
+                const V3 so = v3(pool[0 * kBlock + owner], pool[1 * kBlock + owner], pool[2 * kBlock + owner]);
+                const V3 sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
+                const float stm = pool[6 * kBlock + owner];
+                int hid = -1;
+                float ht = 0.0f;
+                if (STATS) cn.q0 = cn.nodes;
+                bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
+                    g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
+                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
+                if (P.n_sph > 0 && !hit) {
+                    for (int k = 0; k < P.n_sph; ++k) {
+                        float root;
+                        if (sphere_hit(P.sph[k], so, sd, kTMin, stm, root)) { hit = true; break; }
+                    }
+                }
+                // the result travels back in the owner's t_max word: NaN = occluded
+                pool[6 * kBlock + owner] = hit ? __int_as_float(0x7FC00000) : 0.0f;
+            }
+            __builtin_amdgcn_s_setprio(0);
+        }
+        PRT_CLOCK(2);
+        __syncthreads();
+        PRT_CLOCK(3);
+        // ------------------------------------------------------------------ R: resolve
+        if (item >= 0) {
+            if (my_sh) {
+                const float r = pool[6 * kBlock + tid];
+                if (r == r) L = L + pend;   // not occluded
+                my_sh = false;
+                ++bounce;
+                if (bounce >= P.depth) {
+                    float* out = P.out + (size_t)item * 3;
+                    out[0] = L.x; out[1] = L.y; out[2] = L.z;
+                    if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
+                    item = -1;
+                }
+            }
+        }
+        // the next extension ray: origin from the pool slot, direction wi (assigned on every lane,
+        // idle ones included, so that no register keeps the previous ray across the S phase)
+        o = v3(pool[0 * kBlock + tid], pool[1 * kBlock + tid], pool[2 * kBlock + tid]);
+        d = wi;
+        const bool alive = ctl[2 + parity] != 0u;
+        parity ^= 1;
+        if (!alive) break;
+    }
+#ifdef PRT_POOL_CLOCKS
+    if (lane == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 24 + k, (unsigned long long)ck[k]);
+#endif
+#undef PRT_CLOCK
+    if (STATS) {
+        uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
+        for (int off = 32; off > 0; off >>= 1) {
+            a += __shfl_down(a, off); b += __shfl_down(b, off);
+            c += __shfl_down(c, off); e += __shfl_down(e, off);
+        }
+        uint64_t ph[5] = {n_e, n_s, lanes_s, pre_hits, 0};
+        for (int k = 0; k < 4; ++k)
+            for (int off = 32; off > 0; off >>= 1) ph[k] += __shfl_down(ph[k], off);
+        if (lane == 0) {
+            atomicAdd(P.stats + 0, (unsigned long long)a);
+            atomicAdd(P.stats + 1, (unsigned long long)b);
+            atomicAdd(P.stats + 2, (unsigned long long)c);
+            atomicAdd(P.stats + 3, (unsigned long long)e);
+            // diag 17..20 (pool kernel): wave E iterations, wave S iterations, lanes of the S
+            // iterations, shadow rays answered by the light-triangle test
+            for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, (unsigned long long)ph[k]);
+        }
+        uint32_t msp = cn.max_sp, nf = cn.nonfinite, mq = cn.max_q;
+        for (int off = 32; off > 0; off >>= 1) {
+            msp = max(msp, (uint32_t)__shfl_down((int)msp, off));
+            nf += (uint32_t)__shfl_down((int)nf, off);
+            mq = max(mq, (uint32_t)__shfl_down((int)mq, off));
+        }
+        if (lane == 0) {
+            atomicMax(P.stats + 13, (unsigned long long)msp);
+            if (nf) atomicAdd(P.stats + 14, (unsigned long long)nf);
+            atomicMax(P.stats + 16, (unsigned long long)mq);
+        }
+    }
+}
+
 }  // namespace
 
 // variant table: (VAR bits of trace_kernel, LDS-resident scene, min waves per SIMD); see prt_kernels.h
+// (bit 512: the block-pooled shadow-query kernel trace_kernel_pool)
 #define PRT_VARIANTS(X)                       \
     X(kVarLds, 8, true, 7)                    \
     X(kVarLdsAnyOcc, 8, true, 1)              \
     X(kVarGlobal, 224, false, 6)              \
     X(kVarLdsMis, 256, true, 6)               \
     X(kVarLds6, 8, true, 6)                   \
-    X(kVarGlobalMis, 480, false, 6)
+    X(kVarGlobalMis, 480, false, 6)           \
+    X(kVarLdsPool, 512, true, 7)              \
+    X(kVarLdsPool6, 512, true, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
 static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStream_t stream) {
     constexpr bool spill = (VAR & 32) != 0;
-    if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
+    if constexpr ((VAR & 512) != 0) {
+        // the pool kernel's LDS stack size is a launch parameter (P.lds_stack): one instantiation,
+        // compiled in its own unit (prt_trace_pool.hip, other register-allocation flags)
+        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, grid, smem, stream);
+        else return hipErrorInvalidValue;
+    } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
         trace_kernel<STACK, STATS, VAR, LDS, WPE><<<grid, kBlock, smem, stream>>>(P);
         return hipGetLastError();
     } else {
@@ -1398,7 +1880,9 @@ static hipError_t launch_var(const TraceParams& P, int var, int grid, size_t sme
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
 static void occ_one(int* n, size_t smem) {
     constexpr bool spill = (VAR & 32) != 0;
-    if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
+    if constexpr ((VAR & 512) != 0) {
+        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, smem);
+    } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(n, trace_kernel<STACK, STATS, VAR, LDS, WPE>, kBlock, smem);
 }
 

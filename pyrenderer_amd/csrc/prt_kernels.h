@@ -53,6 +53,7 @@ struct TraceParams {
     // counter (16 B at `work`), bit 1 the watchdog flag (first chunk of a render only) — instead of
     // two memset launches per frame
     int cam_clears;
+    int lds_stack;            // pool kernel: 16-bit LDS traversal stack entries per lane (>= the BVH4's need)
 };
 
 // trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the
@@ -68,8 +69,12 @@ constexpr int kVarLdsMis = 4;      // LDS scene, mixed schedule, >= 6 waves/SIMD
 constexpr int kVarGlobalMis = 5;   // kVarGlobal + MIS
 constexpr int kVarLds6 = 6;        // kVarLds built for >= 6 waves/SIMD (80 VGPRs): LDS scenes whose copy
                                    // fits six blocks per CU but not seven
+constexpr int kVarLdsPool = 7;     // LDS-resident scene, block-pooled shadow queries (trace_kernel_pool),
+                                   // >= 7 waves/SIMD; the LDS stack size is P.lds_stack
+constexpr int kVarLdsPool6 = 8;    // kVarLdsPool built for >= 6 waves/SIMD (80 VGPRs)
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 6;
+constexpr int kVarLast = 8;
+bool variant_pool(int var);
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
@@ -94,5 +99,8 @@ hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, b
 hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_slots, int log_tw, int log_tpx, int x0,
                           int y0, int w, int h, float* out, hipStream_t stream);
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
+// the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
+hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream);
+int trace_occ_pool(bool stats, int wpe, size_t smem);
 
 }  // namespace prt

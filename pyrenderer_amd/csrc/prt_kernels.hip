@@ -227,6 +227,12 @@ size_t lds_scene_bytes(const TraceParams& P) {
 }
 
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
+    if (variant_pool(var)) {
+        // trace_kernel_pool: 16-bit stacks of P.lds_stack entries, the shadow pool, queue and control
+        // words, then the BVH4 octant copies, triangles and light records (no shading data)
+        return (size_t)P.lds_stack * kBlock * sizeof(short) + 16 * (size_t)(kPoolF4 + kQueueF4 + kCtlF4) +
+               16 * (7 * (size_t)P.n_node_f4 + P.n_tri_f4 + 4 * (size_t)P.n_lt) + 4 * ((size_t)P.n_light + 1);
+    }
     // traversal stack entries: 16-bit for LDS-resident scenes, 32-bit otherwise
     size_t b = (size_t)stack * kBlock * (variant_uses_lds(var) ? sizeof(short) : sizeof(int));
     if (variant_uses_lds(var)) b += lds_scene_bytes(P);
@@ -314,6 +320,15 @@ bool variant_quantized(int var) {
 bool variant_spills(int var) {
     switch (var) {
 #define X(id, bits, lds, wpe) case id: return (bits & 32) != 0;
+        PRT_VARIANTS(X)
+#undef X
+        default: return false;
+    }
+}
+
+bool variant_pool(int var) {
+    switch (var) {
+#define X(id, bits, lds, wpe) case id: return (bits & 512) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;

@@ -121,7 +121,7 @@ def _soup_scene(cornell, n_extra, seed):
     return FlatScene(tri_v, tri_n, tri_mat, tri_prim, lo, hi, f.mat, f.light_tri + n_extra, f.light_off, f.direct_rgb)
 
 
-@pytest.mark.parametrize("n_extra", [0, 6, 12, 20, 40])
+@pytest.mark.parametrize("n_extra", [0, 6, 12, 20, 28, 40])
 def test_default_variant_reaches_its_occupancy(cornell, n_extra):
     """The default kernel is chosen by how many blocks' LDS fit one CU: the >= 7-waves LDS build
     (variant 1) must actually get 7 blocks per CU, the >= 6-waves one (variant 6) 6, the global
@@ -133,7 +133,8 @@ def test_default_variant_reaches_its_occupancy(cornell, n_extra):
     flat = _soup_scene(cornell, n_extra, 11) if n_extra else cornell[2]
     ds = DeviceScene(flat, 0)
     var = ds.kernel_info()["variant"]
-    want = {N.VAR_LDS: (7,), N.VAR_LDS6: (6,), N.VAR_GLOBAL: (6,), N.VAR_LDS_ANY_OCC: (1, 2, 3, 4, 5)}
+    want = {N.VAR_LDS_POOL: (7,), N.VAR_LDS: (7,), N.VAR_LDS6: (6,), N.VAR_GLOBAL: (6,),
+            N.VAR_LDS_ANY_OCC: (1, 2, 3, 4, 5)}
     assert var in want, var
     assert ds.blocks_per_cu in want[var], (n_extra, var, ds.blocks_per_cu)
     osc = O.OracleScene.from_flat(flat)
@@ -144,17 +145,17 @@ def test_default_variant_reaches_its_occupancy(cornell, n_extra):
     ds.close()
 
 
-def test_default_variants_cover_both_lds_builds(cornell):
-    """Among the scenes above, both LDS builds are defaults somewhere (the 6-wave build is not
-    dead code)."""
+def test_default_variants_cover_the_lds_builds(cornell):
+    """Among the scenes above, the pooled-shadow kernel (Cornell) and the phase-aligned LDS builds
+    (scenes whose pool copy no longer fits seven blocks) are each the default somewhere."""
     from pyrenderer_amd import _native as N
     from pyrenderer_amd.device_scene import DeviceScene
     seen = set()
-    for n_extra in (0, 6, 12, 20):
+    for n_extra in (0, 6, 12, 20, 28, 40):
         ds = DeviceScene(_soup_scene(cornell, n_extra, 11) if n_extra else cornell[2], 0)
         seen.add(ds.kernel_info()["variant"])
         ds.close()
-    assert {N.VAR_LDS, N.VAR_LDS6} <= seen, seen
+    assert N.VAR_LDS_POOL in seen and ({N.VAR_LDS, N.VAR_LDS6} & seen), seen
 
 
 def test_triangle_soup_matches_oracle(cornell):

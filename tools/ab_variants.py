@@ -39,6 +39,10 @@ def main():
     from pyrenderer_amd.io_utils.read_tungsten import read_file
     scene, cam = read_file(os.path.join(ROOT, "pyrenderer_amd", "media", "cornell-box", "scene.json"))
     flat = flatten_scene(scene)
+    if a.scene == "specular":
+        from pyrenderer_amd.scenes import CORNELL_SPECULAR
+        scene, cam = read_file(CORNELL_SPECULAR)
+        flat = flatten_scene(scene)
     if a.scene == "cubes":
         from pyrenderer_amd.scenes import instanced_cubes
         scene, cam = instanced_cubes()
@@ -71,6 +75,17 @@ def main():
         ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, PRT_FLAG_STATS | vflags(v))
         dg = ds.diag_words(22).astype(np.float64)   # 17..21: ext / shadow iteration clocks, counts, lanes
         tot = dg[4] + dg[5] + dg[6]
+        if v.rstrip("np") in ("7", "8"):
+            # trace_kernel_pool's diag words 17..20: wave E iterations, wave S iterations, lanes of the
+            # S iterations, shadow rays answered by the light-triangle test
+            print(json.dumps({"variant": v, "pool": {
+                "e_wave_iters": int(dg[17]), "s_wave_iters": int(dg[18]),
+                "lanes_per_s_iter": round(dg[19] / max(dg[18], 1), 2),
+                "s_iters_per_e_iter": round(dg[18] / max(dg[17], 1), 3),
+                "shadow_queries": int(dg[3]), "answered_by_light_test": int(dg[20]),
+                "nodes_per_sample": round(dg[0] / samples, 2), "tris_per_sample": round(dg[1] / samples, 2),
+                "max_stack": int(dg[13])}}), flush=True)
+            continue
         print(json.dumps({"variant": v, "diag": {"refill_frac": round(dg[4] / tot, 3), "trav_frac": round(dg[5] / tot, 3),
                                                  "shade_frac": round(dg[6] / tot, 3), "wave_iters": int(dg[7]),
                                                  "lanes_per_iter": round(dg[8] / max(dg[7], 1), 2),
