@@ -1461,17 +1461,22 @@ void trace_kernel_pool(TraceParams P) {
     float4* st4 = sn + 56 * n_node4;
     float4* slv = st4 + P.n_tri_f4;
     int* slo = reinterpret_cast<int*>(slv + 4 * P.n_lt);
+    float4* smt = slv + 4 * P.n_lt + (P.n_light + 4) / 4;   // materials, after the light offsets
     copy_octant_nodes(sn, P.nodes, n_node4);
     for (int i = tid; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
     for (int i = tid; i < 4 * P.n_lt; i += kBlock) slv[i] = P.light_v[i];
     for (int i = tid; i <= P.n_light; i += kBlock) slo[i] = P.light_off[i];
+    for (int i = tid; i < 2 * P.n_mat; i += kBlock) smt[i] = reinterpret_cast<const float4*>(P.mats)[i];
     if (tid < 6) ctl[tid] = 0u;
     __syncthreads();
     const float4* g_nodes = sn;
     const float4* g_tris = st4;
+    // normals and shading frames come from global memory (L1-resident): with either the LDS copy
+    // no longer fits seven blocks per CU at config 2; the materials sit in LDS (C2 -1.3 %, C3
+    // -1.8 % against global loads, profiles/r03/s9/)
     const float4* s_nm = P.tri_nm;
     const float4* s_fr = P.tri_frame;
-    const float* s_mats = P.mats;
+    const float* s_mats = reinterpret_cast<const float*>(smt);
 
     uint32_t q_next = 0, q_end = 0;
     bool exhausted = false;

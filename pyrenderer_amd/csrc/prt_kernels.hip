@@ -231,7 +231,8 @@ size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
         // trace_kernel_pool: 16-bit stacks of P.lds_stack entries, the shadow pool, queue and control
         // words, then the BVH4 octant copies, triangles and light records (no shading data)
         return (size_t)P.lds_stack * kBlock * sizeof(short) + 16 * (size_t)(kPoolF4 + kQueueF4 + kCtlF4) +
-               16 * (7 * (size_t)P.n_node_f4 + P.n_tri_f4 + 4 * (size_t)P.n_lt) + 4 * ((size_t)P.n_light + 1);
+               16 * (7 * (size_t)P.n_node_f4 + P.n_tri_f4 + 4 * (size_t)P.n_lt + ((size_t)P.n_light + 4) / 4 +
+                     2 * (size_t)P.n_mat);
     }
     // traversal stack entries: 16-bit for LDS-resident scenes, 32-bit otherwise
     size_t b = (size_t)stack * kBlock * (variant_uses_lds(var) ? sizeof(short) : sizeof(int));
