@@ -27,6 +27,7 @@ VAR_LDS6 = 6          # VAR_LDS built for >= 6 waves/SIMD (LDS copies that fit 6
 VAR_LDS_POOL = 7      # LDS-resident scene, block-pooled shadow queries (trace_kernel_pool)
 VAR_LDS_POOL6 = 8     # VAR_LDS_POOL built for >= 6 waves/SIMD
 VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6)
+VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6)
 VAR_LAST = 8
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2

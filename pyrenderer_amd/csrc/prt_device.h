@@ -1492,7 +1492,7 @@ void trace_kernel_pool(TraceParams P) {
     int parity = 0;
 #ifdef PRT_POOL_CLOCKS
     // diagnostic build (tools/pool_clocks.py): wave-level cycles in E, at barrier 1, in S, at barrier 2
-    uint64_t ck[4] = {0, 0, 0, 0};
+    uint64_t ck[6] = {0, 0, 0, 0, 0, 0};
     uint64_t t_c = __builtin_amdgcn_s_memtime();
 #define PRT_CLOCK(k) do { const uint64_t t_n = __builtin_amdgcn_s_memtime(); ck[k] += t_n - t_c; t_c = t_n; } while (0)
 #else
@@ -1569,6 +1569,7 @@ void trace_kernel_pool(TraceParams P) {
     while (true) {
         // ------------------------------------------------------------------ E phase
         refill();
+        PRT_CLOCK(4);
         if (__ballot(item >= 0) != 0) {
             if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_e++;
             if (item >= 0) {
@@ -1591,6 +1592,7 @@ void trace_kernel_pool(TraceParams P) {
                     }
                     ht = best;
                 }
+                PRT_CLOCK(5);
                 bool finished = false;
                 if (!hit) {
                     finished = true;
@@ -1810,7 +1812,7 @@ void trace_kernel_pool(TraceParams P) {
     }
 #ifdef PRT_POOL_CLOCKS
     if (lane == 0)
-        for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 24 + k, (unsigned long long)ck[k]);
+        for (int k = 0; k < 6; ++k) atomicAdd(P.stats + 24 + k, (unsigned long long)ck[k]);
 #endif
 #undef PRT_CLOCK
     if (STATS) {

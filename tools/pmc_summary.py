@@ -30,7 +30,7 @@ import os
 import re
 import statistics
 
-EXCLUDE = r"trace_kernel<\d+, true"   # the STATS (instrumented) instantiation
+EXCLUDE = r"trace_kernel(_pool)?<(\d+, )?true"   # the STATS (instrumented) instantiations
 
 
 def per_dispatch(d, kernel="trace_kernel"):

@@ -1,7 +1,7 @@
 """Where the block-pooled kernel's waves spend their time (diagnostic): a library copy built with
--DPRT_POOL_CLOCKS accumulates wave-level s_memtime cycles per phase — E (refill, extension query,
-shading), waiting at barrier 1, S (pooled shadow queries), waiting at barrier 2 — into diag words
-24..27.  One process, config 2, variant 7.
+-DPRT_POOL_CLOCKS accumulates wave-level s_memtime cycles per phase — E (refill / extension query /
+shading + enqueue), waiting at barrier 1, S (pooled shadow queries, or the refill of waves without an S
+chunk), waiting at barrier 2 — into diag words 24..29.  One process, config 2, variant 7.
 
     python -m pyrenderer_amd.build --out abtmp/libprt_clk.so -D PRT_POOL_CLOCKS
     python tools/pool_clocks.py --lib abtmp/libprt_clk.so
@@ -48,12 +48,13 @@ def main():
     for flags in (N.PRT_FLAG_STATS, 0):   # the STATS render zeroes the diag words, the clock build adds to 24..27
         N.check(L.prt_render_tiles(h, N.ptr(cam), W, H, 64, 64, N.ptr(ids), len(ids), cfg["spp"], cfg["depth"], 0,
                                    flags | (a.variant << 8), N.ptr(out), N.ptr(st)))
-    w = np.zeros(28, np.uint64)
-    N.check(L.prt_diag_words(h, N.ptr(w), 28))
-    ck = w[24:28].astype(np.float64)
+    w = np.zeros(30, np.uint64)
+    N.check(L.prt_diag_words(h, N.ptr(w), 30))
+    ck = w[24:30].astype(np.float64)
     tot = ck.sum()
+    names = ("E_shade_enqueue", "barrier1", "S", "barrier2", "E_refill", "E_traversal")
     print(json.dumps({"variant": a.variant, "config": a.config, "wave_cycles": float(tot),
-                      "frac": {k: round(float(v / tot), 4) for k, v in zip(("E", "barrier1", "S", "barrier2"), ck)}}))
+                      "frac": {k: round(float(v / tot), 4) for k, v in zip(names, ck)}}))
     L.prt_scene_destroy(h)
 
 

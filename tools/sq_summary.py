@@ -8,7 +8,7 @@ import re
 import sys
 
 
-def load(dirs, kernel="trace_kernel", exclude=r"trace_kernel<\d+, true"):
+def load(dirs, kernel="trace_kernel", exclude=r"trace_kernel(_pool)?<(\d+, )?true"):
     acc = {}
     for d in dirs:
         for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
