@@ -329,7 +329,8 @@ def main():
         # roofline of the dominant kernel (trace_kernel) on rank 0 (per launch)
         per_rank = 1.0 / world
         n_px_rank = len(my_tiles) * T * T
-        kinfo = ds.kernel_info()
+        # the variant of this workload's launches (small launches take the phase-aligned kernel)
+        kinfo = ds.kernel_info(n_items=int(round(n_px_rank * args.spp / launches_per_step)))
         if args.variant:
             kinfo = dict(kinfo, variant=args.variant)
         # SURVEY.md §8(d) algorithmic bytes per launch (module constants S8_*)

@@ -222,10 +222,14 @@ int prt_hit_all(void* scene, const float* rays, int64_t n, uint64_t seed, uint32
  * the render calls.  Runs the persistent trace kernel of prt_render_tiles.  Synchronous. */
 int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_t seed, uint32_t flags,
                    float* out_rgb);
-/* trace-kernel variant chosen for this scene when flags select none:
+/* trace-kernel variant chosen for this scene's large launches when flags select none:
  * out4 = {variant, BVH arity (2 or 4), bit 0 scene LDS-resident | bit 1 quantised nodes,
- *         LDS traversal stack entries per lane} */
+ *         LDS traversal stack entries per lane (instantiation set)} */
 int prt_scene_kernel(void* scene, int32_t* out4);
+/* the same for one trace launch of n_items (pixel, sample) work items with these render flags: an
+ * LDS-resident scene takes the block-pooled shadow kernel (7) for launches of at least two items
+ * per resident lane and the phase-aligned one (1) below that (e.g. config 1's 65 k samples) */
+int prt_launch_kernel(void* scene, int64_t n_items, uint32_t flags, int32_t* out4);
 /* counters of the last render call made with PRT_FLAG_STATS (synchronises) */
 int prt_last_stats(void* scene, uint64_t* stats4);
 /* diagnostic words of the same call (16 x u64): the 4 counters above, then

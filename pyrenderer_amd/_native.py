@@ -59,6 +59,7 @@ EXPORTS = {
     "prt_scene_create": (_i, [_i, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
     "prt_scene_info": (_i, [_vp, _vp]),
     "prt_scene_kernel": (_i, [_vp, _vp]),
+    "prt_launch_kernel": (_i, [_vp, _i64, _u32, _vp]),
     "prt_closest_hits": (_i, [_vp, _vp, ctypes.c_int64, _u32, _vp, _vp]),
     "prt_hit_all": (_i, [_vp, _vp, _i64, _u64, _u32, _vp]),
     "prt_trace_rays": (_i, [_vp, _vp, _i64, _i, _u64, _u32, _vp]),

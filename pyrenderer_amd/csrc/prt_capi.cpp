@@ -268,14 +268,18 @@ bool lds_fits4(const Scene* s) {
 // kernel: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal tails,
 // >= 6 waves/SIMD (C4: 28.6 ms at 5 waves, 27.2 at 6, 28.6 at 7 with spills).
 // An LDS-resident scene whose pooled-shadow kernel still fits seven blocks per CU takes that kernel
-// (C2 4.13 vs 4.28 ms, C3 at 32 spp 9.70 vs 10.10 ms, profiles/r03/s7/).
-int default_variant(const Scene* s) {
+// for launches of at least two work items per resident lane (C2 4.06 vs 4.28 ms, C3 73.6 vs 77.5 ms,
+// profiles/r03/pool/); smaller launches keep the phase-aligned kernel, whose waves run without
+// block barriers (C1's 65 k items on 459 k lanes: 0.1155 vs 0.1224 ms per launch, profiles/r03/c1ab/).
+int default_variant(const Scene* s, int64_t n_items = INT64_MAX) {
     if (!lds_fits4(s) || !s->stack4) return prt::kVarGlobal;
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
     scene_sizes(s, P);
     P.lds_stack = s->need4;
-    if (s->need4 <= 32 && prt::trace_smem_bytes(16, prt::kVarLdsPool, P) * 7 <= 160 * 1024) return prt::kVarLdsPool;
+    const int64_t lanes = (int64_t)7 * s->cus * 256;
+    if (s->need4 <= 32 && prt::trace_smem_bytes(16, prt::kVarLdsPool, P) * 7 <= 160 * 1024 && n_items >= 2 * lanes)
+        return prt::kVarLdsPool;
     size_t smem = prt::trace_smem_bytes(s->stack4, prt::kVarLds, P);
     return smem * 7 <= 160 * 1024 ? prt::kVarLds : smem * 6 <= 160 * 1024 ? prt::kVarLds6 : prt::kVarLdsAnyOcc;
 }
@@ -317,12 +321,20 @@ void scene_params(Scene* s, prt::TraceParams& P) {
 // Kernel variant (flags or the scene's default), its traversal stack, the blocks per CU of
 // the persistent grid and the spill area of the global variants; switches P to the quantised
 // nodes for the variants that read them.
-int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, prt::TraceParams& P, int* var_out, int* stack_out,
-                int* occ_out) {
-    const bool stats = (flags & PRT_FLAG_STATS) != 0;
+// the variant a launch of n_items work items takes when the flags name none
+int launch_variant(const Scene* s, uint32_t flags, int64_t n_items) {
     int var = (int)((flags >> PRT_FLAG_VARIANT_SHIFT) & 0xFFu);
     const bool mis = (flags & PRT_FLAG_MIS_NEE) != 0;
-    if (var == 0) var = !mis ? default_variant(s) : (lds_fits4(s) && s->stack4) ? prt::kVarLdsMis : prt::kVarGlobalMis;
+    if (var == 0)
+        var = !mis ? default_variant(s, n_items) : (lds_fits4(s) && s->stack4) ? prt::kVarLdsMis : prt::kVarGlobalMis;
+    return var;
+}
+
+int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, int64_t n_items, prt::TraceParams& P, int* var_out,
+                int* stack_out, int* occ_out) {
+    const bool stats = (flags & PRT_FLAG_STATS) != 0;
+    const bool mis = (flags & PRT_FLAG_MIS_NEE) != 0;
+    int var = launch_variant(s, flags, n_items);
     if (var < prt::kVarFirst || var > prt::kVarLast) return fail(PRT_ERR_ARG, "unknown kernel variant");
     if (prt::variant_mis(var) != mis)
         return fail(PRT_ERR_ARG, "PRT_FLAG_MIS_NEE must be set exactly for the MIS estimator variants");
@@ -448,7 +460,7 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     P.fault = (int*)((char*)cx->work.p + kFaultOffset);
     P.out = (float*)cx->buf.p;
     int var = 0, stack = 0, occ = 0;
-    if (int rc = trace_setup(s, cx, flags, P, &var, &stack, &occ)) return rc;
+    if (int rc = trace_setup(s, cx, flags, chunk * n_slots, P, &var, &stack, &occ)) return rc;
     int64_t n_chunks = (spp + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
     int k = s->ev_used / 2;
@@ -884,7 +896,7 @@ int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_
     P.fault = (int*)((char*)cx->work.p + kFaultOffset);
     P.out = (float*)d_out.p;
     int var = 0, stack = 0, occ = 0;
-    if (int rc = trace_setup(s, cx, flags, P, &var, &stack, &occ)) return rc;
+    if (int rc = trace_setup(s, cx, flags, n_pad, P, &var, &stack, &occ)) return rc;
     const bool stats = (flags & PRT_FLAG_STATS) != 0;
     if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), s->stream));
     HIP_TRY(hipMemsetAsync(cx->work.p, 0, 64, s->stream));   // work counter and watchdog flag
@@ -899,10 +911,13 @@ int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_
     return PRT_OK;
 }
 
-int prt_scene_kernel(void* scene, int32_t* out4) {
+int prt_scene_kernel(void* scene, int32_t* out4) { return prt_launch_kernel(scene, INT64_MAX, 0, out4); }
+
+int prt_launch_kernel(void* scene, int64_t n_items, uint32_t flags, int32_t* out4) {
     auto* s = (Scene*)scene;
     if (!s || !out4) return fail(PRT_ERR_ARG, "NULL argument");
-    int var = default_variant(s);
+    if (n_items < 0) return fail(PRT_ERR_ARG, "n_items < 0");
+    int var = launch_variant(s, flags, n_items);
     out4[0] = var;
     out4[1] = 4;
     out4[2] = (prt::variant_uses_lds(var) ? 1 : 0) | (prt::variant_quantized(var) ? 2 : 0);

@@ -182,10 +182,14 @@ class DeviceScene:
         N.check(N.lib().prt_trace_rays(self.h, N.ptr(rays), rays.shape[0], int(depth), int(seed), flags, N.ptr(out)))
         return out
 
-    def kernel_info(self):
-        """Default trace-kernel variant: dict(variant, bvh_arity, lds_scene, quantized, stack)."""
+    def kernel_info(self, n_items=None, flags=0):
+        """Trace-kernel variant of a launch of n_items work items (default: a large one) with these
+        render flags: dict(variant, bvh_arity, lds_scene, quantized, stack)."""
         out = np.zeros(4, np.int32)
-        N.check(N.lib().prt_scene_kernel(self.h, N.ptr(out)))
+        if n_items is None:
+            N.check(N.lib().prt_scene_kernel(self.h, N.ptr(out)))
+        else:
+            N.check(N.lib().prt_launch_kernel(self.h, int(n_items), flags, N.ptr(out)))
         return dict(variant=int(out[0]), bvh_arity=int(out[1]), lds_scene=bool(out[2] & 1),
                     quantized=bool(out[2] & 2), stack=int(out[3]))
 
