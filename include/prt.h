@@ -227,8 +227,9 @@ int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_
  *         LDS traversal stack entries per lane (instantiation set)} */
 int prt_scene_kernel(void* scene, int32_t* out4);
 /* the same for one trace launch of n_items (pixel, sample) work items with these render flags: an
- * LDS-resident scene takes the block-pooled shadow kernel (7) for launches of at least two items
- * per resident lane and the phase-aligned one (1) below that (e.g. config 1's 65 k samples) */
+ * LDS-resident scene takes the block-pooled shadow kernel (7) for launches of at least eight items
+ * per resident lane and the phase-aligned one (1) below that (config 1's 65 k samples, an 8-rank
+ * shard of config 2) */
 int prt_launch_kernel(void* scene, int64_t n_items, uint32_t flags, int32_t* out4);
 /* counters of the last render call made with PRT_FLAG_STATS (synchronises) */
 int prt_last_stats(void* scene, uint64_t* stats4);

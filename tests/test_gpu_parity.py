@@ -464,11 +464,13 @@ def test_mis_variant_on_the_specular_scene():
 
 def test_launch_size_selects_the_pooled_kernel(gpu_scene):
     """prt_launch_kernel: on the Cornell box a large launch (config 2: 16.8 M items) takes the
-    block-pooled shadow kernel, config 1's 65 k items the phase-aligned one (block barriers do
-    not pay with fewer than two items per resident lane); explicit variant flags win."""
+    block-pooled shadow kernel, config 1's 65 k items and an 8-rank shard of config 2 the
+    phase-aligned one (block barriers do not pay with fewer than eight items per resident lane);
+    explicit variant flags win."""
     from pyrenderer_amd import _native as N
     assert gpu_scene.kernel_info()["variant"] == N.VAR_LDS_POOL
     assert gpu_scene.kernel_info(n_items=512 * 512 * 64)["variant"] == N.VAR_LDS_POOL
     assert gpu_scene.kernel_info(n_items=128 * 128 * 4)["variant"] == N.VAR_LDS
+    assert gpu_scene.kernel_info(n_items=512 * 512 * 64 // 8)["variant"] == N.VAR_LDS   # an 8-rank shard
     assert gpu_scene.kernel_info(n_items=128 * 128 * 4, flags=N.VAR_LDS_POOL << 8)["variant"] == N.VAR_LDS_POOL
     assert gpu_scene.kernel_info(n_items=512 * 512 * 64, flags=N.PRT_FLAG_MIS_NEE)["variant"] == N.VAR_MIS[0]
