@@ -1449,7 +1449,6 @@ void trace_kernel_pool(TraceParams P) {
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
     const int stack_f4 = P.lds_stack * kBlock * 2 / 16;
     LdsStack16 stk;
     stk.l = reinterpret_cast<short*>(smem) + (tid & ~63) + 2 * (tid & 31) + ((tid >> 5) & 1);

@@ -350,6 +350,27 @@ def test_spill_stack_matches_oracle(cornell, oracle_scene, monkeypatch):
     assert np.array_equal(g, o)
 
 
+@pytest.mark.parametrize("variant", ["lds", "global"])
+def test_bvh4_collapse_choice_keeps_the_image(cornell, oracle_scene, monkeypatch, variant):
+    """The SAH-optimal BVH4 collapse (default) and the greedy one (PRT_BVH4_DP=0) give the
+    oracle's image bit for bit, and the optimal one visits no more nodes."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
+    cam = cornell[1].convert_to_taichi_camera().packed()
+    ids = interleaved_tiles(64, 64, 32)
+    o = oracle_scene.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, seed=5)
+    flags = N.PRT_FLAG_STATS | ((N.VAR_GLOBAL << 8) if variant == "global" else 0)
+    visits = {}
+    for dp in ("0", "1"):
+        monkeypatch.setenv("PRT_BVH4_DP", dp)
+        ds = DeviceScene(cornell[2], 0)
+        g, st = ds.render_tiles(cam, 64, 64, 32, 32, ids, 4, 8, 5, flags)
+        assert np.array_equal(g, o), dp
+        visits[dp] = int(st[0])
+        ds.close()
+    assert visits["1"] <= visits["0"], visits
+
+
 def test_large_frame_matches_oracle(gpu_scene, oracle_scene, cornell):
     """1024^2 x 32 spp (33.5 M samples): contains shadow rays with t_max = NaN
     (p2.x == p.x), which once made BVH4 empty slots (then ref = root) 'hit' and the
