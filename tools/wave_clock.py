@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--spp", type=int, default=None, help="override the config's samples per pixel")
     a = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "wave_clock.bin")
     os.environ["PRT_WAVE_CLOCK"] = path
@@ -63,7 +64,7 @@ def main():
     for rep in range(a.reps):
         if os.path.exists(path):
             os.remove(path)
-        ds.render_tiles(cam, W, H, 64, 64, ids, cfg["spp"], cfg["depth"], 0, PRT_FLAG_TIME | (a.variant << 8))
+        ds.render_tiles(cam, W, H, 64, 64, ids, a.spp or cfg["spp"], cfg["depth"], 0, PRT_FLAG_TIME | (a.variant << 8))
         ms, n = ds.kernel_timing()
         raw = np.fromfile(path, dtype=np.uint64).reshape(-1, 3)
         per = raw.shape[0] // max(n, 1)
