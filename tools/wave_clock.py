@@ -34,6 +34,7 @@ def summarise(rec):
     items = rec[:, 2].astype(np.float64)
     return {"waves": int(rec.shape[0]), "span_us": round(float(span), 1),
             "start_spread_us": round(float(st.max()), 1),
+            "start_pct_us": [round(float(np.percentile(st, q)), 1) for q in (25, 50, 57, 60, 75, 90)],
             "end_first_us": round(float(en.min()), 1), "end_p10_us": round(float(np.percentile(en, 10)), 1),
             "end_median_us": round(float(np.median(en)), 1), "end_p90_us": round(float(np.percentile(en, 90)), 1),
             "us_below_50pct_waves": round(float((frac[1:] < 0.5).sum() * dt), 1),
