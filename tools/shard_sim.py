@@ -26,6 +26,15 @@ def main():
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--streams", type=int, default=1, help="frames in flight, as bench.py --streams")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--proxy", default="none", choices=("none", "stream", "stream-hp", "stream-nowait", "inline"),
+                    help="after each frame, a copy of its tile buffer standing in for the RCCL gather: 'stream' on "
+                         "one extra stream, ordered as torch's ProcessGroupNCCL orders a collective (the extra stream "
+                         "waits for the frame, the frame's stream waits for the copy); 'inline' on the frame's own "
+                         "stream (a gather enqueued on the render stream); 'stream-hp' as 'stream' on a high-priority "
+                         "stream (TORCH_NCCL_HIGH_PRIORITY=1); 'stream-nowait' as 'stream' without the frame stream's "
+                         "wait (timing only)")
+    ap.add_argument("--no-null-stream", action="store_true",
+                    help="render every frame on a created stream (default: the first on torch's current stream)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -42,10 +51,30 @@ def main():
     ds = DeviceScene(flat, 0)
     W = H = cfg["res"]
     dev = torch.device("cuda", 0)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(a.streams - 1)]
+    streams = ([] if a.no_null_stream else [torch.cuda.current_stream(dev)])
+    streams += [torch.cuda.Stream(dev) for _ in range(a.streams - len(streams))]
+    coll = (torch.cuda.Stream(dev, priority=-1) if a.proxy == "stream-hp" else
+            torch.cuda.Stream(dev) if a.proxy in ("stream", "stream-nowait") else None)
+
+    def gather_proxy(buf, st, dst):
+        if a.proxy == "inline":
+            with torch.cuda.stream(st):
+                dst.copy_(buf)
+        if coll is None:
+            return
+        ev = torch.cuda.Event()
+        ev.record(st)
+        coll.wait_event(ev)
+        with torch.cuda.stream(coll):
+            dst.copy_(buf)
+        if a.proxy != "stream-nowait":
+            done = torch.cuda.Event()
+            done.record(coll)
+            st.wait_event(done)
 
     def time_tiles(tile, ids):
         bufs = [torch.empty(max(len(ids), 1) * tile * tile * 3, dtype=torch.float32, device=dev) for _ in streams]
+        dst = torch.empty_like(bufs[0])
         for b, st in zip(bufs, streams):
             ds.render_tiles_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], b.data_ptr(), st.cuda_stream,
                                    flags=a.variant << 8)
@@ -56,6 +85,7 @@ def main():
             k = i % len(streams)
             ds.render_tiles_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], bufs[k].data_ptr(),
                                    streams[k].cuda_stream, flags=N.PRT_FLAG_TIME | (a.variant << 8))
+            gather_proxy(bufs[k], streams[k], dst)
         torch.cuda.synchronize(dev)
         wall = (time.perf_counter() - t0) * 1e3 / a.steps
         kms, launches = ds.kernel_timing()
@@ -63,7 +93,7 @@ def main():
 
     for tile in [int(t) for t in a.tiles.split(",")]:
         t1_wall, t1_k = time_tiles(tile, interleaved_tiles(W, H, tile))
-        print(json.dumps({"tile": tile, "world": 1, "streams": a.streams, "variant": a.variant, "wall_ms": round(t1_wall, 4), "kernel_ms": round(t1_k, 4)}),
+        print(json.dumps({"tile": tile, "world": 1, "streams": a.streams, "proxy": a.proxy, "variant": a.variant, "wall_ms": round(t1_wall, 4), "kernel_ms": round(t1_k, 4)}),
               flush=True)
         for scheme in a.schemes.split(","):
             for world in [int(w) for w in a.worlds.split(",")]:
@@ -73,7 +103,7 @@ def main():
                     walls.append(w)
                     kerns.append(k)
                 print(json.dumps({
-                    "tile": tile, "scheme": scheme, "world": world, "streams": a.streams,
+                    "tile": tile, "scheme": scheme, "world": world, "streams": a.streams, "proxy": a.proxy,
                     "max_tiles": max_tiles_per_rank(W, H, tile, world, scheme),
                     "wall_ms": [round(x, 4) for x in walls], "kernel_ms": [round(x, 4) for x in kerns],
                     "kernel_max_over_mean": round(max(kerns) / (sum(kerns) / world), 4),
