@@ -94,6 +94,10 @@ def parse():
                     help="frames in flight (1 = strictly serial frames; 0 = auto: 3 when a rank renders < 8 M "
                          "samples per frame, else 2 on several GPUs and 1 on one)")
     ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
+    ap.add_argument("--frames-per-launch", type=int, default=0,
+                    help="frames per render call (prt_render_frames_device: their items share the persistent "
+                         "launches, one ramp-up and drain per call); 0 = auto: min(steps, 16), 1 for frames of "
+                         "> 64 M samples per rank")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N > 1: nccl (= RCCL over xGMI, the default) or gloo "
                          "(tile sums staged through host memory; rehearses the N > 1 path with several ranks "
@@ -228,8 +232,59 @@ def l2_vs_cpu(gpu_sums, ids, cpu_sums, args):
             "reference": "oracle/prt_oracle.c (C port of PathTracer.trace), same seed, random 8x8 tiles"}
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_check(args, env=None):
+    """The N-GPU launch contract, checked before anything touches a GPU (torch.cuda.device_count()
+    does not initialise the device on this image).  Returns None when this process should
+    render, else an exit code: a child launcher's, or 2 for a mislaunch.
+
+    * `--gpus N > 1` without a launcher (no WORLD_SIZE): start `torch.distributed.run` with N
+      ranks on this node as a CHILD process (never exec: the parent has not touched the GPU,
+      but the child must own it), forward its output and exit with its code.
+    * under a launcher: WORLD_SIZE must equal --gpus, and for --backend nccl (RCCL: one rank per
+      device) N must not exceed the visible devices — either mismatch would print a plausible
+      line for the wrong N."""
+    env = os.environ if env is None else env
+    import torch
+    n_dev = torch.cuda.device_count()
+    if args.gpus < 1:
+        print(f"bench.py: --gpus must be >= 1 (got {args.gpus})", file=sys.stderr)
+        return 2
+    if args.backend == "nccl" and args.gpus > 1 and args.gpus > n_dev:
+        print(f"bench.py: --gpus {args.gpus} with --backend nccl needs {args.gpus} devices, "
+              f"{n_dev} visible", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in env:
+        if args.gpus == 1:
+            return None
+        import subprocess
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+               os.path.abspath(__file__)] + sys.argv[1:]
+        child_env = dict(env, HSA_ENABLE_IPC_MODE_LEGACY=env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        sys.stdout.flush()
+        return subprocess.run(cmd, env=child_env).returncode
+    world = int(env["WORLD_SIZE"])
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch N ranks for --gpus N",
+              file=sys.stderr)
+        return 2
+    return None
+
+
 def main():
     args = parse()
+    rc = launch_check(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
 
@@ -265,6 +320,14 @@ def main():
     t_build = time.perf_counter() - t_build
     W = H = args.res
     T = args.tile if args.tile else (64 if world == 1 else 16)
+    rank_samples = W * H * args.spp / world
+    # frames per render call (prt_render_frames_device): F frames' (pixel, sample) items run through
+    # the same persistent launches, so a launch ramps up and drains once per F frames instead of once
+    # per frame; each frame is still rendered, reduced, gathered and scattered whole
+    F = args.frames_per_launch
+    if F <= 0:
+        F = min(args.steps, 16) if rank_samples <= 64e6 else 1
+    F = max(1, min(F, args.steps))
     n_streams = args.streams
     if n_streams <= 0:
         # measured (profiles/r01/shard_sim_*, streams_ab): for a whole C2 frame on one GPU,
@@ -275,25 +338,42 @@ def main():
         # tail is a larger share: 3 frames in flight (0.741 vs 0.777 ms per frame at 1/8).
         # On several GPUs the per-launch roofline is not the headline, and overlap pays more (a
         # half frame at N = 2: 2.55 vs 2.65 ms with 2 streams, profiles/r01/shard_sim_c2_streams_t16.jsonl).
-        rank_samples = W * H * args.spp / world
-        n_streams = 3 if rank_samples < 8e6 else (2 if world > 1 else 1)
+        # Multi-frame launches already amortise the drain: serial launches.
+        n_streams = 1 if F > 1 else (3 if rank_samples < 8e6 else (2 if world > 1 else 1))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
-    shards = [TileShard(W, H, T, rank, world, dev, args.scheme, host_staging=gloo) for _ in range(n_streams)]
+    shards = [TileShard(W, H, T, rank, world, dev, args.scheme, host_staging=gloo, frames=F) for _ in range(n_streams)]
     my_tiles = shards[0].tiles
     n_step = [0]
+    rflags = (args.variant << 8) | (N.PRT_FLAG_NO_PRIMARY_KERNEL if args.no_primary_kernel else 0)
 
-    def step(flags=0):
+    def steps(nf, flags=0):
+        """nf (<= F) steps: nf frames rendered by one render call, then each frame's gather to rank 0
+        and (root) its device scatter into the (W, H, 3) frame."""
         k = n_step[0] % n_streams
         n_step[0] += 1
         shard, stream = shards[k], streams[k]
-        ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, shard.buf.data_ptr(),
-                               stream.cuda_stream, seed=args.seed,
-                               flags=flags | (args.variant << 8) | (N.PRT_FLAG_NO_PRIMARY_KERNEL if args.no_primary_kernel else 0))
+        if nf == 1:
+            ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, shard.buf.data_ptr(),
+                                   stream.cuda_stream, seed=args.seed, flags=flags | rflags)
+        else:
+            ds.render_frames_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, nf, shard.bufs.data_ptr(),
+                                    stream.cuda_stream, seed=args.seed, frame_stride=0, flags=flags | rflags)
         with torch.cuda.stream(stream):
-            shard.gather()    # RCCL gather of per-tile radiance sums to rank 0 (ordered after this frame)
+            shard.gather(n_frames=nf)    # RCCL gathers of per-tile radiance sums to rank 0 (ordered after the frames)
+            if world > 1 and rank == 0:
+                # root: every rank's tiles into the (W, H, 3) device frames (SURVEY.md §8(e)), inside the step
+                for f in range(nf):
+                    shard.scatter(ds, stream, f)
 
+    def run(n):
+        while n > 0:
+            nf = min(F, n)
+            steps(nf, N.PRT_FLAG_TIME if timing[0] else 0)
+            n -= nf
+
+    timing = [False]
     # counted traversal work of one frame (deterministic: same RNG as the timed steps)
-    step(N.PRT_FLAG_STATS)
+    steps(1, N.PRT_FLAG_STATS)
     torch.cuda.synchronize(dev)
     st = np.append(ds.last_stats().astype(np.float64), float(ds.diag_stats()[14]))
     cnt = torch.tensor(st, dtype=torch.float64, device=coll_dev)
@@ -301,14 +381,14 @@ def main():
         dist.all_reduce(cnt)
     nodes, tris, ext, shadow, nonfinite = cnt.tolist()
 
-    for _ in range(args.warmup):
-        step()
+    # warmup: the W steps, and at least one full group of F frames (its buffers are then allocated)
+    run(max(args.warmup, F))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    timing[0] = True
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(N.PRT_FLAG_TIME)
+    run(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -335,7 +415,8 @@ def main():
             kinfo = dict(kinfo, variant=args.variant)
         # SURVEY.md §8(d) algorithmic bytes per launch (module constants S8_*)
         work_launch = per_rank / launches_per_step
-        bytes_launch = (S8_NODE * nodes + S8_TRI * tris + S8_LIGHT * shadow) * work_launch + S8_PIXEL * n_px_rank
+        bytes_launch = ((S8_NODE * nodes + S8_TRI * tris + S8_LIGHT * shadow) * work_launch
+                        + S8_PIXEL * n_px_rank / launches_per_step)
         kern_s = kern_avg_ms * 1e-3
         achieved = bytes_launch / kern_s / 1e9
         # what the kernel really reads per launch from its scene copy (LDS for LDS-resident scenes)
@@ -389,14 +470,18 @@ def main():
         hbm_logical = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_launch": int(bytes_launch)}
         if kinfo["lds_scene"]:
-            # the scene sits in LDS: §8(d)'s algorithmic bytes are LDS reads (their figure against
-            # the HBM peak can pass 1), and what binds is VALU issue under divergence
+            # the scene sits in LDS: §8(d)'s algorithmic bytes are LDS reads, not HBM traffic, and
+            # what binds is VALU issue under divergence
             roofline = dict({"bound": "valu", "achieved": round(flops_tf, 3), "peak": VALU_PEAK_TFLOPS,
                              "unit": "TFLOP/s", "frac": round(flops_tf / VALU_PEAK_TFLOPS, 4),
                              "flops_per_launch": int(flops_launch)}, **common)
-            roofline["hbm_logical"] = dict(hbm_logical, note="SURVEY.md §8(d) algorithmic bytes (32 B per node "
-                                           "visit, 48 per triangle test, 48 per shadow query's light point, 12 per "
-                                           "pixel) against the HBM peak; served from LDS here, so not an HBM bound")
+            # §8(d)'s byte accounting, kept as a rate only: priced against the HBM peak it would read
+            # above 1 although none of these bytes reach HBM (the `lds` block prices them correctly)
+            roofline["s8d_bytes_from_lds"] = {
+                "rate": round(achieved, 2), "unit": "GB/s", "bytes_per_launch": int(bytes_launch),
+                "note": "SURVEY.md §8(d) algorithmic bytes (32 B per node visit, 48 per triangle test, 48 per "
+                        "shadow query's light point, 12 per pixel) over the kernel duration; served from the "
+                        "LDS scene copy, so not an HBM figure (HBM: traffic / hbm_measured_frac)"}
             roofline["lds"] = {"achieved": round(scene_gbs, 2), "peak": LDS_PEAK_GBS, "unit": "GB/s",
                                "frac": round(scene_gbs / LDS_PEAK_GBS, 4),
                                "note": "bytes read from the LDS scene copy (112 B per f32 BVH4 node, 48 per "
@@ -427,7 +512,7 @@ def main():
                        "baseline_config": args.config, "triangles": int(flat.n_tri), "spheres": int(flat.sph.shape[0]),
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
                        "backend": (args.backend if world > 1 else None),
-                       "tile_scheme": args.scheme, "frames_in_flight": n_streams,
+                       "tile_scheme": args.scheme, "frames_in_flight": n_streams, "frames_per_launch": F,
                        "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
             "roofline": roofline,
             "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),

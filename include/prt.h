@@ -29,8 +29,9 @@ extern "C" {
 #endif
 
 /* ABI 2 (this build): prt_trace_rays, prt_hit_all added; trace-kernel variant ids renumbered
- * to 1..6 (PRT_FLAG_VARIANT; ABI 1's ids 7..33 are rejected with PRT_ERR_ARG and its 1..6
- * named other kernels, so a caller built against ABI 1 must check prt_abi_version());
+ * to 1..8 (PRT_FLAG_VARIANT; 7 / 8 are the pooled-shadow kernel; ids above 8 are rejected with
+ * PRT_ERR_ARG, and ABI 1's ids 1..8 named other kernels, so a caller built against ABI 1 must
+ * check prt_abi_version());
  * prt_scene_info's info8[4] is the BVH4 LDS traversal stack depth (0: BVH4 too deep for
  * the LDS-stack variants); watchdog flags are cleared once reported (prt_check_faults). */
 #define PRT_ABI_VERSION 2
@@ -58,7 +59,8 @@ extern "C" {
  * kVar* table of pyrenderer_amd/csrc/prt_kernels.h: 1 LDS-resident scene (>= 7 waves per
  * SIMD), 2 the same without an occupancy target, 3 global scene (quantised nodes, spill
  * stack), 4 / 5 the MIS estimator on an LDS / global scene, 6 the LDS-resident scene built
- * for >= 6 waves per SIMD).  Variants of one estimator produce
+ * for >= 6 waves per SIMD, 7 / 8 the LDS-resident block-pooled shadow kernel for >= 7 / >= 6
+ * waves per SIMD).  Variants of one estimator produce
  * bit-identical images; the selector exists for A/B runs and tests. */
 #define PRT_FLAG_VARIANT_SHIFT 8
 #define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFFu) << PRT_FLAG_VARIANT_SHIFT)
@@ -159,7 +161,10 @@ void prt_comm_release(void);
  * packed tile sums d_packed (device, n_tiles*tw*th x 3 f32, slot order of prt_render_tiles) of the
  * host tile ids `tile_ids` -> the device frame d_frame (W x H x 3 f32, [x][y]; slots outside the
  * frame are dropped, pixels of other tiles untouched), one kernel enqueued on `stream` (NULL = the
- * scene's stream, whose device is used).  Replaces a host-side unpack of the gathered buffers. */
+ * scene's stream, whose device is used).  A tile id of -1 marks a padding slot (a rank with fewer
+ * tiles than the gather buffer's per-rank stride): its pixels are dropped.  The tile origins are
+ * uploaded only when the tile set differs from the previous call's.  Replaces a host-side unpack
+ * of the gathered buffers. */
 int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_ids, int n_tiles, int tw, int th,
                       int W, int H, float* d_frame, void* stream);
 /* Progressive rendering: main_taichi.py:108-127 runs render() once per GUI frame
@@ -182,6 +187,18 @@ int prt_render_tiles_accumulate(void* scene, const float* cam, int W, int H, int
 int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw, int th,
                             const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
                             uint32_t flags, float* d_out_sum, void* stream);
+/* Several frames through the same persistent launches (the progressive frame loop of
+ * main_taichi.py:108-118, or repeated renders of one frame): frame f = samples
+ * f * frame_stride + 0 .. spp - 1 of every pixel of the tile set (frame_stride = spp: consecutive
+ * progressive frames; 0: n_frames renders of the same samples), its per-pixel sums written to
+ * d_out_sums + f * n_tiles*tw*th*3 (device, slot order of prt_render_tiles).  Every frame is
+ * bit-identical to the prt_render_tiles_accumulate call of its samples from zero sums; the
+ * launches carry all frames' (pixel, sample) items (as many frames per launch as the per-launch
+ * buffer budget holds), so a persistent launch ramps up and drains once per launch instead of
+ * once per frame.  Enqueued on `stream` like prt_render_tiles_device. */
+int prt_render_frames_device(void* scene, const float* cam, int W, int H, int tw, int th,
+                             const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
+                             int n_frames, int frame_stride, uint32_t flags, float* d_out_sums, void* stream);
 /* trace-kernel time of every render call made with PRT_FLAG_TIME since the
  * previous prt_kernel_timing() (synchronises on their events, then resets):
  * total ms and number of trace launches.  Also reports PRT_ERR_INTERNAL if the
@@ -224,7 +241,8 @@ int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_
                    float* out_rgb);
 /* trace-kernel variant chosen for this scene's large launches when flags select none:
  * out4 = {variant, BVH arity (2 or 4), bit 0 scene LDS-resident | bit 1 quantised nodes,
- *         LDS traversal stack entries per lane (instantiation set)} */
+ *         LDS traversal stack entries per lane: the instantiation set, or for the pooled kernel
+ *         (7 / 8) the exact BVH4 bound its stack is sized to} */
 int prt_scene_kernel(void* scene, int32_t* out4);
 /* the same for one trace launch of n_items (pixel, sample) work items with these render flags: an
  * LDS-resident scene takes the block-pooled shadow kernel (7) for launches of at least eight items

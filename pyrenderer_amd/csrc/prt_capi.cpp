@@ -139,8 +139,8 @@ struct Scene {
     // of every rank and their tile origins (host copy kept alive for the async upload)
     DevBuf frame, gather, gather_xy;
     std::vector<uint32_t> gather_xy_host;
-    // prt_scatter_tiles: tile origins of the last call (host copy alive until its upload has run,
-    // i.e. until scatter_ev completes)
+    // prt_scatter_tiles: tile origins of the last upload (host copy alive until it has run, i.e.
+    // until scatter_ev completes; re-uploaded only when a call's tile set differs)
     DevBuf scatter_xy;
     std::vector<uint32_t> scatter_xy_host;
     hipEvent_t scatter_ev = nullptr;
@@ -318,6 +318,7 @@ void scene_params(Scene* s, prt::TraceParams& P) {
     P.n_sph = (int)s->n_sph;
     P.sph = (const float4*)s->sph.p;
     P.sph_mat = (const int*)s->sph_mat.p;
+    P.frame_spp = 0xFFFFFFFFu;   // one frame: global sample = s0 + j0 + the chunk's sample
 }
 
 // Kernel variant (flags or the scene's default), its traversal stack, the blocks per CU of
@@ -379,9 +380,13 @@ int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, int64_t n_items, prt::T
 // Enqueue the whole render of a tile set on `stream`, result in d_acc: samples
 // first_sample .. first_sample + spp - 1 of every pixel; `accumulate` adds them onto the
 // sums already in d_acc (progressive rendering) instead of overwriting them.
+// n_frames > 1 (prt_render_frames_device): frame f renders samples first_sample + f * frame_stride
+// + 0 .. spp - 1 into d_acc + f * n_slots * 3, and all frames' items run through the same
+// persistent launches (a launch covers up to the memory budget's worth of frames), so the
+// launch drains once per launch instead of once per frame.
 int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
                    int n_tiles, int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc,
-                   int first_sample = 0, bool accumulate = false) {
+                   int first_sample = 0, bool accumulate = false, int n_frames = 1, int frame_stride = 0) {
     const int64_t n_slots = (int64_t)n_tiles * tw * th;
     if (n_slots == 0) return PRT_OK;
     hipStream_t stream = cx->stream;
@@ -401,9 +406,11 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     }
     if (spp == 0 || depth == 0) {
         // every sample's radiance is 0: the sums are 0, or unchanged when accumulating
-        if (!accumulate) HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots, stream));
+        if (!accumulate) HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots * n_frames, stream));
         return PRT_OK;
     }
+    // the launches' sample space: j = f * spp + (sample of frame f), T of them
+    const int64_t T = (int64_t)spp * n_frames;
     // per-sample buffers: radiance (12 B) + primary ray (16 B, pinhole cameras)
     const bool cam_fast = camera_is_fast(cam);
     const bool primary = cam_fast && !(flags & PRT_FLAG_NO_PRIMARY_KERNEL);
@@ -417,17 +424,17 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     {
         const size_t held = cx->buf.bytes + cx->rays.bytes;
         size_t free_b = 0, total_b = 0;
-        if ((size_t)(std::min<int64_t>(spp, (int64_t)(budget / (size_t)per_sample_all)) * per_sample_all) > held &&
+        if ((size_t)(std::min<int64_t>(T, (int64_t)(budget / (size_t)per_sample_all)) * per_sample_all) > held &&
             hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
             budget = std::min(budget, std::max<size_t>((size_t)per_sample_all, (free_b + held) / 2));
     }
-    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(spp, (int64_t)budget / per_sample_all));
+    int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)budget / per_sample_all));
     // keep every chunk's item count below 2^31 (32-bit work counter)
     chunk = std::min<int64_t>(chunk, std::max<int64_t>(1, ((int64_t)1 << 31) / n_slots - 1));
     // equal launches: no short last launch paying a whole launch tail for a few samples
     {
-        const int64_t nc = (spp + chunk - 1) / chunk;
-        chunk = (spp + nc - 1) / nc;
+        const int64_t nc = (T + chunk - 1) / chunk;
+        chunk = (T + nc - 1) / nc;
     }
     HIP_TRY(cx->buf.ensure((size_t)(chunk * per_sample)));
     if (primary) HIP_TRY(cx->rays.ensure((size_t)(chunk * n_slots * 16)));
@@ -461,9 +468,12 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     P.work = (uint32_t*)cx->work.p;
     P.fault = (int*)((char*)cx->work.p + kFaultOffset);
     P.out = (float*)cx->buf.p;
+    P.s0 = first_sample;
+    P.frame_spp = (uint32_t)spp;
+    P.frame_stride = (uint32_t)frame_stride;
     int var = 0, stack = 0, occ = 0;
     if (int rc = trace_setup(s, cx, flags, chunk * n_slots, P, &var, &stack, &occ)) return rc;
-    int64_t n_chunks = (spp + chunk - 1) / chunk;
+    int64_t n_chunks = (T + chunk - 1) / chunk;
     // timed launches accumulate event pairs until prt_kernel_timing() reads them
     int k = s->ev_used / 2;
     if (timed) {
@@ -474,9 +484,9 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         }
         s->ev_used += (int)(2 * n_chunks);
     }
-    for (int64_t s0 = 0; s0 < spp; s0 += chunk, ++k) {
-        int64_t n = std::min<int64_t>(chunk, spp - s0);
-        P.s0 = first_sample + (int)s0;   // global sample index: keys the RNG streams
+    for (int64_t s0 = 0; s0 < T; s0 += chunk, ++k) {
+        int64_t n = std::min<int64_t>(chunk, T - s0);
+        P.j0 = (uint32_t)s0;   // launch sample offset: keys the RNG streams through global_sample()
         P.n_items = (uint64_t)(n * n_slots);
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
@@ -510,8 +520,13 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
             }
             P.wave_clock = nullptr;
         }
-        HIP_TRY(prt::launch_reduce((const float*)cx->buf.p, d_acc, (int)n_slots, (int)n, s0 == 0 && !accumulate,
-                                   stream));
+        // per frame overlapping the chunk: its samples [a, b) of the launch sample space, in order
+        for (int64_t f = s0 / spp; f < n_frames && f * spp < s0 + n; ++f) {
+            const int64_t a = std::max<int64_t>(s0, f * spp), b = std::min<int64_t>(s0 + n, (f + 1) * spp);
+            HIP_TRY(prt::launch_reduce((const float*)cx->buf.p + (size_t)(a - s0) * n_slots * 3,
+                                       d_acc + (size_t)f * n_slots * 3, (int)n_slots, (int)(b - a),
+                                       a == f * spp && !accumulate, stream));
+        }
     }
     return PRT_OK;
 }
@@ -871,9 +886,15 @@ int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_
     if (n_tiles > 65535) return fail(PRT_ERR_ARG, "too many rays in one call (<= 65535 x 64)");
     std::vector<uint32_t> origins((size_t)n_tiles);
     for (int64_t t = 0; t < n_tiles; ++t) origins[(size_t)t] = (uint32_t)t;
-    HIP_TRY(cx->tiles.ensure(sizeof(uint32_t) * (size_t)n_tiles));
-    HIP_TRY(hipMemcpy(cx->tiles.p, origins.data(), sizeof(uint32_t) * (size_t)n_tiles, hipMemcpyHostToDevice));
-    cx->tile_host.clear();   // the next tile render re-uploads its own origins
+    if (origins != cx->tile_host) {
+        // enqueued on the context's stream, behind any render still running there (an unsynchronised
+        // prt_render_tiles_device reads the old origins until it ends); the host copy lives in
+        // cx->tile_host until the next upload, as enqueue_render's
+        HIP_TRY(cx->tiles.ensure(sizeof(uint32_t) * (size_t)n_tiles));
+        HIP_TRY(hipMemcpyAsync(cx->tiles.p, origins.data(), sizeof(uint32_t) * (size_t)n_tiles,
+                               hipMemcpyHostToDevice, cx->stream));
+        cx->tile_host.swap(origins);
+    }
     DevBuf d_in, d_org, d_out;
     HIP_TRY(d_in.ensure(sizeof(float) * 8 * (size_t)n));
     HIP_TRY(d_org.ensure(sizeof(float) * 4 * (size_t)n_pad));
@@ -923,7 +944,8 @@ int prt_launch_kernel(void* scene, int64_t n_items, uint32_t flags, int32_t* out
     out4[0] = var;
     out4[1] = 4;
     out4[2] = (prt::variant_uses_lds(var) ? 1 : 0) | (prt::variant_quantized(var) ? 2 : 0);
-    out4[3] = variant_stack(s, var);
+    // the pooled kernel's LDS stack is sized to the BVH4's exact bound (P.lds_stack = need4)
+    out4[3] = prt::variant_pool(var) ? s->need4 : variant_stack(s, var);
     return PRT_OK;
 }
 
@@ -997,6 +1019,24 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
     RenderCtx* cx = ctx_for(s, stream ? (hipStream_t)stream : s->stream);
     if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
     return enqueue_render(s, cx, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, d_out_sum);
+}
+
+int prt_render_frames_device(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
+                             int n_tiles, int spp, int depth, uint64_t seed, int n_frames, int frame_stride,
+                             uint32_t flags, float* d_out_sums, void* stream) {
+    auto* s = (Scene*)scene;
+    int rc = check_render_args(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth);
+    if (rc) return rc;
+    if (n_frames < 1) return fail(PRT_ERR_ARG, "n_frames must be >= 1");
+    if (frame_stride < 0) return fail(PRT_ERR_ARG, "frame_stride must be >= 0");
+    if ((int64_t)(n_frames - 1) * frame_stride + spp > INT32_MAX || (int64_t)n_frames * spp > INT32_MAX)
+        return fail(PRT_ERR_ARG, "sample indices must stay below 2^31");
+    if (!d_out_sums && n_tiles > 0) return fail(PRT_ERR_ARG, "d_out_sums is NULL");
+    DeviceGuard g(s->device);
+    RenderCtx* cx = ctx_for(s, stream ? (hipStream_t)stream : s->stream);
+    if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
+    return enqueue_render(s, cx, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, d_out_sums, 0, false,
+                          n_frames, frame_stride);
 }
 
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
@@ -1115,26 +1155,38 @@ int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_id
     if (W < 1 || H < 1 || W > 65535 || H > 65535) return fail(PRT_ERR_ARG, "frame must be 1..65535 pixels per side");
     const int tiles_x = (W + tw - 1) / tw, tiles_y = (H + th - 1) / th;
     for (int i = 0; i < n_tiles; ++i)
-        if (tile_ids[i] < 0 || tile_ids[i] >= tiles_x * tiles_y)
+        if (tile_ids[i] < -1 || tile_ids[i] >= tiles_x * tiles_y)
             return fail(PRT_ERR_ARG, "tile id out of range: " + std::to_string(tile_ids[i]));
     if ((int64_t)n_tiles * tw * th >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many slots in one call");
     if (n_tiles == 0) return PRT_OK;
     DeviceGuard g(s->device);
     hipStream_t st = stream ? (hipStream_t)stream : s->stream;
-    // the previous call's upload must have run before its host copy / device buffer are reused
-    if (s->scatter_ev) HIP_TRY(hipEventSynchronize(s->scatter_ev));
-    else HIP_TRY(hipEventCreateWithFlags(&s->scatter_ev, hipEventDisableTiming));
-    s->scatter_xy_host.resize((size_t)n_tiles);
+    // tile origins (x0 << 16 | y0); a padding slot (id -1) gets x0 = 0xFFFF, past any frame's
+    // width (<= 65535), so the kernel drops its pixels
+    std::vector<uint32_t> xy((size_t)n_tiles);
     for (int i = 0; i < n_tiles; ++i)
-        s->scatter_xy_host[(size_t)i] =
-            ((uint32_t)((tile_ids[i] % tiles_x) * tw) << 16) | (uint32_t)((tile_ids[i] / tiles_x) * th);
-    HIP_TRY(s->scatter_xy.ensure(sizeof(uint32_t) * (size_t)n_tiles));
-    HIP_TRY(hipMemcpyAsync(s->scatter_xy.p, s->scatter_xy_host.data(), sizeof(uint32_t) * (size_t)n_tiles,
-                           hipMemcpyHostToDevice, st));
+        xy[(size_t)i] = tile_ids[i] < 0 ? 0xFFFF0000u
+                                        : ((uint32_t)((tile_ids[i] % tiles_x) * tw) << 16) |
+                                              (uint32_t)((tile_ids[i] / tiles_x) * th);
+    // uploaded only when they differ from the last call's (a bench or an animation scatters the
+    // same tile set every frame): a steady-state frame then neither copies nor waits on the host
+    if (xy != s->scatter_xy_host) {
+        // earlier scatters (on any stream) may still read the device copy, and the previous
+        // upload its host copy: a changed tile set waits for the device once
+        if (s->scatter_ev) HIP_TRY(hipDeviceSynchronize());
+        else HIP_TRY(hipEventCreateWithFlags(&s->scatter_ev, hipEventDisableTiming));
+        HIP_TRY(s->scatter_xy.ensure(sizeof(uint32_t) * (size_t)n_tiles));
+        s->scatter_xy_host.swap(xy);
+        HIP_TRY(hipMemcpyAsync(s->scatter_xy.p, s->scatter_xy_host.data(), sizeof(uint32_t) * (size_t)n_tiles,
+                               hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(s->scatter_ev, st));
+    } else if (hipEventQuery(s->scatter_ev) != hipSuccess) {
+        // same tile set, uploaded on a stream that may not have reached the copy yet
+        HIP_TRY(hipStreamWaitEvent(st, s->scatter_ev, 0));
+    }
     const int log_tw = __builtin_ctz((unsigned)tw), log_tpx = __builtin_ctz((unsigned)(tw * th));
     HIP_TRY(prt::launch_scatter(d_packed, (const uint32_t*)s->scatter_xy.p, n_tiles * tw * th, log_tw, log_tpx, 0, 0, W,
                                 H, d_frame, st));
-    HIP_TRY(hipEventRecord(s->scatter_ev, st));
     return PRT_OK;
 }
 

@@ -663,6 +663,16 @@ __device__ __forceinline__ void pixel_of(const TraceParams& P, uint32_t item, ui
     y = (int)(xy0 & 0xFFFFu) + (int)(loc >> log_tw);
 }
 
+// Global sample index (the RNG key's sample) of the launch's chunk-relative sample `chunk_s`:
+// frame f = j / frame_spp of a multi-frame launch renders samples f * frame_stride + (j % frame_spp)
+// (TraceParams::j0).  Wave-uniform operands: one scalar division per chunk or camera wave.
+__device__ __forceinline__ uint32_t global_sample(const TraceParams& P, uint32_t chunk_s) {
+    uint32_t j = P.j0 + chunk_s, fs = P.frame_spp, st = P.frame_stride, s0 = (uint32_t)P.s0;
+    asm volatile("" : "+s"(fs), "+s"(st), "+s"(s0));
+    const uint32_t f = j / fs;
+    return s0 + f * st + (j - f * fs);
+}
+
 // Camera sample for pixel (x, y) of sample `chunk_s` (main_taichi.py:89-95): RNG key,
 // jitter, gen_ray.
 __device__ __forceinline__ void camera_ray(const TraceParams& P, int x, int y, uint32_t chunk_s, uint32_t& st, V3& o,
@@ -670,7 +680,7 @@ __device__ __forceinline__ void camera_ray(const TraceParams& P, int x, int y, u
     int W = P.W;
     float wm1 = P.wm1, hm1 = P.hm1;
     asm volatile("" : "+s"(W), "+s"(wm1), "+s"(hm1));
-    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)W + (uint32_t)x, (uint32_t)P.s0 + chunk_s);
+    st = rng_key(P.seed_lo, P.seed_hi, (uint32_t)y * (uint32_t)W + (uint32_t)x, global_sample(P, chunk_s));
     float r0 = rng_next(st);
     float u = ((float)x + r0) / wm1;
     float r1 = rng_next(st);

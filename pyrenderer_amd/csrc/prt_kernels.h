@@ -35,7 +35,12 @@ struct TraceParams {
     int log_tw, log_tpx;      // log2(tile width), log2(tile pixels): tiles are powers of two, >= 64 px
     const uint32_t* tile_xy;  // per tile of this launch: (x0 << 16) | y0
     int n_slots;              // n_tiles * tw * th
-    int s0;                   // first sample index of this chunk
+    int s0;                   // first sample index of the render (keys the RNG streams with the frame mapping below)
+    // several frames in one launch (prt_render_frames_device): the launch's sample index j (chunk
+    // offset j0 + the item's sample within the chunk) is sample j % frame_spp of frame j / frame_spp,
+    // whose samples start at frame * frame_stride; global sample = s0 + that.  One frame:
+    // frame_spp > every j, so the global sample is s0 + j.
+    uint32_t j0, frame_spp, frame_stride;
     int depth;
     uint32_t seed_lo, seed_hi;
     uint64_t n_items;         // n_slots * samples in this chunk

@@ -149,6 +149,17 @@ class DeviceScene:
                                                 spp, depth, int(seed), flags, ctypes.c_void_p(d_out_ptr),
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def render_frames_device(self, cam, W, H, tw, th, tile_ids, spp, depth, n_frames, d_out_ptr, stream_ptr=None,
+                             seed=0, frame_stride=0, flags=0):
+        """prt_render_frames_device: n_frames frames through the same persistent launches; frame f
+        (samples f * frame_stride + 0..spp-1) -> d_out_ptr + f * n_slots * 3 floats.  Enqueued."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        tile_ids = np.ascontiguousarray(tile_ids, np.int32)
+        N.check(N.lib().prt_render_frames_device(self.h, N.ptr(cam), W, H, tw, th, N.ptr(tile_ids),
+                                                 tile_ids.shape[0], spp, depth, int(seed), int(n_frames),
+                                                 int(frame_stride), flags, ctypes.c_void_p(d_out_ptr),
+                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
     def scatter_tiles(self, d_packed_ptr, tile_ids, tw, th, W, H, d_frame_ptr, stream_ptr=None):
         """prt_scatter_tiles: packed tile sums (device) -> the device frame (W, H, 3) [x][y], enqueued."""
         tile_ids = np.ascontiguousarray(tile_ids, np.int32)

@@ -19,57 +19,100 @@ from .device_scene import interleaved_tiles, max_tiles_per_rank, tile_grid, unpa
 class TileShard:
     """This rank's tiles and the padded gather buffers (allocated once).
 
-    `buf` holds the rank's per-tile radiance sums on `device`.  With `host_staging` (the
-    gloo backend, which moves CPU tensors) gather() first copies them to host memory."""
+    `bufs[f]` holds the rank's per-tile radiance sums of frame f (of `frames`, the frames one
+    render call produces: DeviceScene.render_frames_device) on `device`; `buf` is frame 0.  With
+    `host_staging` (the gloo backend, which moves CPU tensors) gather() first copies them to host
+    memory."""
 
-    def __init__(self, W, H, tile, rank, world, device, scheme="latin", host_staging=False):
+    def __init__(self, W, H, tile, rank, world, device, scheme="latin", host_staging=False, frames=1):
         self.W, self.H, self.tile, self.rank, self.world = W, H, tile, rank, world
         self.scheme = scheme
+        self.frames = int(frames)
         tx, ty = tile_grid(W, H, tile)
         self.n_tiles = tx * ty
         self.tiles = interleaved_tiles(W, H, tile, rank, world, scheme)
         self.max_tiles = max_tiles_per_rank(W, H, tile, world, scheme)
         self.slot_elems = tile * tile * 3
-        self.buf = torch.zeros(self.max_tiles * self.slot_elems, dtype=torch.float32, device=device)
+        self.bufs = torch.zeros((self.frames, self.max_tiles * self.slot_elems), dtype=torch.float32, device=device)
+        self.buf = self.bufs[0]
         self.host_staging = bool(host_staging) and self.buf.is_cuda
-        self.wire = torch.empty_like(self.buf, device="cpu") if self.host_staging else self.buf
-        self.gather_list = ([torch.empty_like(self.wire) for _ in range(world)]
-                            if (world > 1 and rank == 0) else None)
+        self.wire = torch.empty_like(self.bufs, device="cpu") if self.host_staging else self.bufs
+        self.gather_lists = None
+        self.gathered = None
+        if world > 1 and rank == 0:
+            # per frame one contiguous receive buffer, rank-major with a stride of max_tiles tiles:
+            # the device scatter then reads every rank's tiles in one kernel (padding slots: id -1)
+            self.gathered = torch.empty((self.frames, world, self.bufs.shape[1]), dtype=torch.float32,
+                                        device=self.wire.device)
+            self.gather_lists = [list(self.gathered[f].unbind(0)) for f in range(self.frames)]
+        self.gather_list = self.gather_lists[0] if self.gather_lists else None
+        self.per_rank = [interleaved_tiles(W, H, tile, r, world, scheme) for r in range(world)]
+        ids = np.full((world, self.max_tiles), -1, np.int32)
+        for r, t in enumerate(self.per_rank):
+            ids[r, :len(t)] = t
+        self.scatter_ids = ids.reshape(-1)
+        self.frame_out = None    # rank 0's device frames (frames, W, H, 3), allocated by scatter()
+        self.packed_dev = None   # gloo: a gathered host buffer's device copy
 
-    def gather(self, group=None):
-        """Collective: rank 0 receives every rank's tile sums (no-op for world 1).  Runs on
-        torch's current stream: callers that rendered on another stream enter it first."""
+    def gather(self, group=None, n_frames=1):
+        """Collective: rank 0 receives every rank's tile sums of frames 0 .. n_frames-1, one
+        gather per frame (no-op for world 1).  Runs on torch's current stream: callers that
+        rendered on another stream enter it first, and a later scatter() on the same stream is
+        ordered after the receive (ProcessGroupNCCL makes the current stream wait for its
+        collective stream when the work is enqueued)."""
         if self.world > 1:
             if self.host_staging:
-                self.wire.copy_(self.buf)       # synchronous device-to-host copy on the current stream
-            dist.gather(self.wire, self.gather_list, dst=0, group=group)
+                self.wire[:n_frames].copy_(self.bufs[:n_frames])   # synchronous device-to-host copy
+            for f in range(n_frames):
+                dist.gather(self.wire[f], self.gather_lists[f] if self.gather_lists else None, dst=0, group=group)
 
-    def assemble(self, device_scene=None, stream=None):
-        """Rank 0: (W, H, 3) float32 sums frame from the gathered buffers.
+    @property
+    def frame(self):
+        return None if self.frame_out is None else self.frame_out[0]
 
-        With `device_scene` (GPU ranks) the tiles are scattered into a device frame by libprt's
-        scatter kernel (prt_scatter_tiles) on `stream` (default: torch's current stream) — the
-        gathered buffers, already on the device over RCCL or uploaded once from gloo's host
-        staging, never pass through a host loop; the frame is then copied to the host.  Without
-        it (CPU-tensor shards: the gloo tests with the CPU oracle as renderer) the tiles are
-        unpacked in numpy."""
-        bufs = self.gather_list if self.world > 1 else [self.buf]
-        per_rank = [interleaved_tiles(self.W, self.H, self.tile, r, self.world, self.scheme) for r in range(self.world)]
+    def scatter(self, device_scene, stream=None, f=0):
+        """Rank 0 after gather(): every rank's tiles of frame f -> the (W, H, 3) device frame
+        `frame_out[f]` by libprt's scatter kernel (prt_scatter_tiles, one launch over the
+        rank-major gathered buffer), enqueued on `stream` (default: torch's current stream).
+        gloo's host buffer is first uploaded on that stream.  This is the root-side step of
+        SURVEY.md §8(e) that bench.py times inside every N > 1 step."""
+        dev = torch.device("cuda", device_scene.device)
+        s = stream or torch.cuda.current_stream(dev)
+        with torch.cuda.stream(s):
+            # the frames are zeroed once: every pixel belongs to exactly one tile, which every
+            # scatter overwrites
+            if self.frame_out is None:
+                self.frame_out = torch.zeros((self.frames, self.W, self.H, 3), dtype=torch.float32, device=dev)
+            if self.world == 1:
+                packed = self.bufs[f]
+            elif self.gathered.is_cuda:
+                packed = self.gathered[f]
+            else:
+                if self.packed_dev is None:
+                    self.packed_dev = torch.empty(self.gathered[0].numel(), dtype=torch.float32, device=dev)
+                self.packed_dev.copy_(self.gathered[f].reshape(-1))
+                packed = self.packed_dev
+        ids = self.scatter_ids if self.world > 1 else self.per_rank[0]
+        device_scene.scatter_tiles(packed.data_ptr(), ids, self.tile, self.tile, self.W, self.H,
+                                   self.frame_out[f].data_ptr(), s.cuda_stream)
+        return self.frame_out[f]
+
+    def assemble(self, device_scene=None, stream=None, f=0):
+        """Rank 0: (W, H, 3) float32 sums of frame f (host) from the gathered buffers.
+
+        With `device_scene` (GPU ranks): scatter() on `stream`, then one device-to-host copy of
+        the frame — the gathered tiles never pass through a host loop.  Without it (CPU-tensor
+        shards: the gloo tests with the CPU oracle as renderer) the tiles are unpacked in numpy."""
         if device_scene is None:
+            bufs = self.gather_lists[f] if self.world > 1 else [self.bufs[f]]
             frame = np.zeros((self.W, self.H, 3), np.float32)
-            for b, ids in zip(bufs, per_rank):
+            for b, ids in zip(bufs, self.per_rank):
                 n = len(ids) * self.slot_elems
                 unpack_tiles(b[:n].cpu().numpy().reshape(-1, 3), self.W, self.H, self.tile, self.tile, ids, frame)
             return frame
         dev = torch.device("cuda", device_scene.device)
         s = stream or torch.cuda.current_stream(dev)
-        with torch.cuda.stream(s):
-            packed = torch.cat([b[:len(ids) * self.slot_elems].to(dev, non_blocking=False)
-                                for b, ids in zip(bufs, per_rank)])
-            frame = torch.zeros((self.W, self.H, 3), dtype=torch.float32, device=dev)
-        ids = np.concatenate(per_rank).astype(np.int32)
-        device_scene.scatter_tiles(packed.data_ptr(), ids, self.tile, self.tile, self.W, self.H, frame.data_ptr(),
-                                   s.cuda_stream)
+        frame = self.scatter(device_scene, s, f)
         with torch.cuda.stream(s):
             out = frame.cpu().numpy()
         return out

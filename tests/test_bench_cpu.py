@@ -56,3 +56,54 @@ def test_host_cpu_and_kernel_sha(monkeypatch):
     assert bench.host_cpu()[0] == aff
     from pyrenderer_amd.build import kernel_sha
     assert kernel_sha() == kernel_sha() and len(kernel_sha()) == 16
+
+
+def _args(monkeypatch, argv):
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    return bench.parse()
+
+
+def test_launch_check_spawns_the_launcher_as_a_child(monkeypatch):
+    """`bench.py --gpus N` without WORLD_SIZE starts torch.distributed.run with N ranks as a child
+    process (subprocess, never exec) and exits with its code."""
+    import subprocess
+    seen = {}
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return types.SimpleNamespace(returncode=7)
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    args = _args(monkeypatch, ["--gpus", "2", "--backend", "gloo", "--steps", "3"])
+    rc = bench.launch_check(args, env={"PATH": "/usr/bin"})
+    assert rc == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=2" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-6:] == ["--gpus", "2", "--backend", "gloo", "--steps", "3"]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # one GPU, or already under a launcher with the matching world size: render in this process
+    assert bench.launch_check(_args(monkeypatch, []), env={}) is None
+    assert bench.launch_check(args, env={"WORLD_SIZE": "2"}) is None
+
+
+def _run_bench(argv, **env):
+    import os
+    import subprocess
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env)
+    return subprocess.run([sys.executable, "bench.py"] + argv, cwd=ROOT, env=e, capture_output=True, text=True,
+                          timeout=120)
+
+
+def test_mislaunch_exits_nonzero_before_any_gpu_call():
+    # WORLD_SIZE != --gpus under a launcher
+    r = _run_bench(["--gpus", "4", "--backend", "gloo"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert r.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in r.stderr, r.stderr
+    # nccl (one rank per device) with more ranks than visible devices (none in this container)
+    import torch
+    n = torch.cuda.device_count() + 1
+    r = _run_bench(["--gpus", str(max(n, 2)), "--backend", "nccl"])
+    assert r.returncode == 2 and "needs" in r.stderr and "visible" in r.stderr, r.stderr
+    r = _run_bench(["--gpus", "0"])
+    assert r.returncode == 2
