@@ -366,10 +366,11 @@ def main():
                     shard.scatter(ds, stream, f)
 
     def run(n):
-        while n > 0:
-            nf = min(F, n)
+        # equal groups of <= F frames (equal launches: the per-launch roofline averages like sizes)
+        groups = -(-n // F)
+        for g in range(groups):
+            nf = n // groups + (1 if g < n % groups else 0)
             steps(nf, N.PRT_FLAG_TIME if timing[0] else 0)
-            n -= nf
 
     timing = [False]
     # counted traversal work of one frame (deterministic: same RNG as the timed steps)

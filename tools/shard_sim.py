@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--streams", type=int, default=1, help="frames in flight, as bench.py --streams")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--frames", type=int, default=1,
+                    help="frames per render call (prt_render_frames_device, bench.py --frames-per-launch); "
+                         "--steps is then a multiple of it")
     ap.add_argument("--proxy", default="none", choices=("none", "stream", "stream-hp", "stream-nowait", "inline"),
                     help="after each frame, a copy of its tile buffer standing in for the RCCL gather: 'stream' on "
                          "one extra stream, ordered as torch's ProcessGroupNCCL orders a collective (the extra stream "
@@ -72,28 +75,39 @@ def main():
             done.record(coll)
             st.wait_event(done)
 
+    F = max(1, a.frames)
+
+    def render(ids, tile, buf, st, flags):
+        if F == 1:
+            ds.render_tiles_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], buf.data_ptr(), st.cuda_stream,
+                                   flags=flags | (a.variant << 8))
+        else:
+            ds.render_frames_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], F, buf.data_ptr(),
+                                    st.cuda_stream, flags=flags | (a.variant << 8))
+
     def time_tiles(tile, ids):
-        bufs = [torch.empty(max(len(ids), 1) * tile * tile * 3, dtype=torch.float32, device=dev) for _ in streams]
-        dst = torch.empty_like(bufs[0])
+        n = max(len(ids), 1) * tile * tile * 3
+        bufs = [torch.empty(F * n, dtype=torch.float32, device=dev) for _ in streams]
+        dst = torch.empty(n, dtype=torch.float32, device=dev)
         for b, st in zip(bufs, streams):
-            ds.render_tiles_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], b.data_ptr(), st.cuda_stream,
-                                   flags=a.variant << 8)
+            render(ids, tile, b, st, 0)
         torch.cuda.synchronize(dev)
         ds.kernel_timing()
+        groups = max(1, a.steps // F)
         t0 = time.perf_counter()
-        for i in range(a.steps):
+        for i in range(groups):
             k = i % len(streams)
-            ds.render_tiles_device(cam, W, H, tile, tile, ids, cfg["spp"], cfg["depth"], bufs[k].data_ptr(),
-                                   streams[k].cuda_stream, flags=N.PRT_FLAG_TIME | (a.variant << 8))
-            gather_proxy(bufs[k], streams[k], dst)
+            render(ids, tile, bufs[k], streams[k], N.PRT_FLAG_TIME)
+            for f in range(F):   # one gather per frame
+                gather_proxy(bufs[k][f * n:(f + 1) * n], streams[k], dst)
         torch.cuda.synchronize(dev)
-        wall = (time.perf_counter() - t0) * 1e3 / a.steps
+        wall = (time.perf_counter() - t0) * 1e3 / (groups * F)
         kms, launches = ds.kernel_timing()
-        return wall, kms / max(launches, 1)
+        return wall, kms / max(launches, 1) / F
 
     for tile in [int(t) for t in a.tiles.split(",")]:
         t1_wall, t1_k = time_tiles(tile, interleaved_tiles(W, H, tile))
-        print(json.dumps({"tile": tile, "world": 1, "streams": a.streams, "proxy": a.proxy, "variant": a.variant, "wall_ms": round(t1_wall, 4), "kernel_ms": round(t1_k, 4)}),
+        print(json.dumps({"tile": tile, "world": 1, "streams": a.streams, "frames": F, "proxy": a.proxy, "variant": a.variant, "wall_ms": round(t1_wall, 4), "kernel_ms": round(t1_k, 4)}),
               flush=True)
         for scheme in a.schemes.split(","):
             for world in [int(w) for w in a.worlds.split(",")]:
@@ -103,7 +117,7 @@ def main():
                     walls.append(w)
                     kerns.append(k)
                 print(json.dumps({
-                    "tile": tile, "scheme": scheme, "world": world, "streams": a.streams, "proxy": a.proxy,
+                    "tile": tile, "scheme": scheme, "world": world, "streams": a.streams, "frames": F, "proxy": a.proxy,
                     "max_tiles": max_tiles_per_rank(W, H, tile, world, scheme),
                     "wall_ms": [round(x, 4) for x in walls], "kernel_ms": [round(x, 4) for x in kerns],
                     "kernel_max_over_mean": round(max(kerns) / (sum(kerns) / world), 4),
