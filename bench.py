@@ -356,8 +356,10 @@ def main():
             ds.render_tiles_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, shard.buf.data_ptr(),
                                    stream.cuda_stream, seed=args.seed, flags=flags | rflags)
         else:
+            # consecutive progressive frames (main_taichi.py:108-118): frame f of the group renders
+            # samples f * spp .. (f + 1) * spp - 1, so no two frames of a launch repeat work
             ds.render_frames_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, nf, shard.bufs.data_ptr(),
-                                    stream.cuda_stream, seed=args.seed, frame_stride=0, flags=flags | rflags)
+                                    stream.cuda_stream, seed=args.seed, frame_stride=args.spp, flags=flags | rflags)
         with torch.cuda.stream(stream):
             shard.gather(n_frames=nf)    # RCCL gathers of per-tile radiance sums to rank 0 (ordered after the frames)
             if world > 1 and rank == 0:

@@ -91,6 +91,10 @@ int prt_bvh_build(const float* tri_v, int64_t n_tri, int32_t max_leaf, void** ou
 int prt_bvh_info(void* bvh, int64_t* info6);
 /* nodes: n_nodes x 16 f32; tris: n_tri x 12 f32 (BVH order); order: n_tri (BVH slot -> triangle) */
 int prt_bvh_export(void* bvh, float* nodes, float* tris, int32_t* order);
+/* The compact BVH4 records the global-scene kernels traverse (one array of 48-B node and
+ * triangle records, 12 f32 each, layout in pyrenderer_amd/csrc/prt_internal.h compact_bvh4):
+ * *n_records is set; the records are copied to out when cap_records >= *n_records.  For tests. */
+int prt_bvh_compact(void* bvh, float* out, int64_t cap_records, int64_t* n_records);
 void prt_bvh_destroy(void* bvh);
 
 /* -------------------------------------------------------------- scene ----

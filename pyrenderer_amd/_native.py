@@ -55,6 +55,7 @@ EXPORTS = {
     "prt_bvh_build": (_i, [_vp, _i64, _i32, _vp]),
     "prt_bvh_info": (_i, [_vp, _vp]),
     "prt_bvh_export": (_i, [_vp, _vp, _vp, _vp]),
+    "prt_bvh_compact": (_i, [_vp, _vp, _i64, _vp]),
     "prt_bvh_destroy": (None, [_vp]),
     "prt_scene_create": (_i, [_i, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
     "prt_scene_info": (_i, [_vp, _vp]),
@@ -141,6 +142,14 @@ class Bvh:
         order = np.zeros(self.n_tri, np.int32)
         check(lib().prt_bvh_export(self.h, ptr(nodes), ptr(tris), ptr(order)))
         return nodes, tris, order
+
+    def compact(self):
+        """The compact BVH4 records of the global-scene kernels: (n_records, 12) float32."""
+        n = ctypes.c_int64(0)
+        check(lib().prt_bvh_compact(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros((n.value, 12), np.float32)
+        check(lib().prt_bvh_compact(self.h, ptr(out), n.value, ctypes.byref(n)))
+        return out
 
     def __del__(self):
         if getattr(self, "h", None):

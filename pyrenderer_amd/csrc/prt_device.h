@@ -471,6 +471,7 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     bool h0, h1, h2, h3;
     int r0, r1, r2, r3;
     if (QN) {
+#ifdef PRT_QN64
         // 64-B nodes at a 32-bit byte offset from the uniform base (saddr + voffset addressing,
         // no 64-bit address arithmetic): BVH4 nodes < refs / 3 < 2^25, so the offset < 2^31
         const float4* nd = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + ((uint32_t)cur << 6));
@@ -487,6 +488,37 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
         h1 = qchild(1, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t1) && r1 != kSentinel;
         h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && r2 != kSentinel;
         h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && r3 != kSentinel;
+#else
+        // compact 48-B records (prt_internal.h compact_bvh4) at a 32-bit byte offset from the
+        // uniform base: three 16-B loads per lane instead of four — the global-scene traversal is
+        // bound by the vector L1's tag lookups (one per distinct line per wave load instruction:
+        // TA / TD busy 0.92 / 0.98 of the C4 launch, profiles/r04/pmc_mem/)
+        const float4* nd = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint32_t)cur * 48u);
+        const float4 a = nd[0], b = nd[1], c = nd[2];
+        if (STATS) { cn.nodes++; cn.it_inner++; }
+        const uint32_t ex = __float_as_uint(c.z), meta = __float_as_uint(c.w), base = __float_as_uint(a.w);
+        // grid steps 2^e from the f32 exponent fields (exact), applied to 1/d like quantize_bvh4's steps
+        const float s_x = __uint_as_float((ex & 0xFFu) << 23), s_y = __uint_as_float(((ex >> 8) & 0xFFu) << 23);
+        const float s_z = __uint_as_float(((ex >> 16) & 0xFFu) << 23);
+        QAxis X = {s_x * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
+        QAxis Y = {s_y * inv.y, __builtin_fmaf(a.y, inv.y, -oi.y)};
+        QAxis Z = {s_z * inv.z, __builtin_fmaf(a.z, inv.z, -oi.z)};
+        uint32_t lxq = __float_as_uint(sx ? b.y : b.x), hxq = __float_as_uint(sx ? b.x : b.y);
+        uint32_t lyq = __float_as_uint(sy ? b.w : b.z), hyq = __float_as_uint(sy ? b.z : b.w);
+        uint32_t lzq = __float_as_uint(sz ? c.y : c.x), hzq = __float_as_uint(sz ? c.x : c.y);
+        // child refs without a load: inner = base + rank, leaf = ~((base << 3) + ((offset << 3) | (count - 1)))
+        const uint32_t fl = ex >> 24;
+        const uint32_t b8 = base << 3;
+        auto ref = [&](int k) {
+            const uint32_t off = (meta >> (8 * k)) & 0xFFu;
+            return (fl >> k) & 1u ? (int)(base + off) : (int)~(b8 + off);
+        };
+        r0 = ref(0); r1 = ref(1); r2 = ref(2); r3 = ref(3);
+        h0 = qchild(0, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t0) && !(fl & 16u);
+        h1 = qchild(1, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t1) && !(fl & 32u);
+        h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && !(fl & 64u);
+        h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && !(fl & 128u);
+#endif
     } else {
         float4 nx, fx, ny, fy, nz, fz, rf;
         if (OCT) {
@@ -609,6 +641,27 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 while (mc > 1 && !__ballot(cnt >= mc)) --mc;
                 if (__builtin_amdgcn_readfirstlane(__lane_id()) == __lane_id()) cn.w_tri += mc;
             }
+#ifdef PRT_TRI_PIPE
+            if constexpr (QN) {
+                // global scenes: the next triangle's record is loaded while this one is tested (one
+                // L2 round trip per leaf instead of one per triangle); the last trip reloads its own
+                const float4* tp = tris + (size_t)first * 3;
+                float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+                for (int k = 0; k < cnt; ++k) {
+                    const float4* tn = tp + 3 * min(k + 1, cnt - 1);
+                    const float4 n0 = tn[0], n1 = tn[1], n2 = tn[2];
+                    int id = __float_as_int(q0.w);
+                    float t;
+                    if (STATS) cn.tris++;
+                    if (mt_u(xyz(q0), xyz(q1), xyz(q2), o, d, tmin, best, id, best_id, any, t)) {
+                        best = t;
+                        best_id = id;
+                        if (any) { cur = S::kSent; break; }
+                    }
+                    q0 = n0; q1 = n1; q2 = n2;
+                }
+            } else
+#endif
             for (int k = 0; k < cnt; ++k) {
                 const float4* tp = tris + (size_t)(first + k) * 3;
                 float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
