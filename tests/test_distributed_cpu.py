@@ -60,3 +60,44 @@ def test_gather_matches_single_process(tmp_path, world, W, H):
                                                                 DEPTH, seed=SEED, tile=TILE)
     np.testing.assert_array_equal(frame, ref)
     assert frame.sum() > 0
+
+
+def _frames_worker(rank, world, port, out_path, n_frames):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, ROOT)
+    from pyrenderer_amd.distributed import TileShard
+    shard = TileShard(W, H, TILE, rank, world, torch.device("cpu"), frames=n_frames)
+    # frame f's sums of pixel (x, y): a value that names both, so a mixed-up frame or tile shows
+    n = len(shard.tiles) * TILE * TILE
+    for f in range(n_frames):
+        vals = np.zeros((n, 3), np.float32)
+        for k, t in enumerate(shard.tiles):
+            tx, ty = t % ((W + TILE - 1) // TILE), t // ((W + TILE - 1) // TILE)
+            for j in range(TILE * TILE):
+                x, y = tx * TILE + j % TILE, ty * TILE + j // TILE
+                vals[k * TILE * TILE + j] = (x, y, f) if (x < W and y < H) else 0.0
+        shard.bufs[f, :n * 3] = torch.from_numpy(vals.reshape(-1))
+    shard.gather(n_frames=n_frames)
+    if rank == 0:
+        np.save(out_path, np.stack([shard.assemble(f=f) for f in range(n_frames)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_frame_gathers(tmp_path, world):
+    """bench.py's multi-frame groups: F frames' tile sums per rank, one gather per frame, each
+    frame assembled from its own gathered buffer."""
+    out = str(tmp_path / "frames.npy")
+    F = 3
+    mp.spawn(_frames_worker, args=(world, _free_port(), out, F), nprocs=world, join=True)
+    frames = np.load(out)
+    assert frames.shape == (F, W, H, 3)
+    x, y = np.meshgrid(np.arange(W), np.arange(H), indexing="ij")
+    for f in range(F):
+        np.testing.assert_array_equal(frames[f][..., 0], x)
+        np.testing.assert_array_equal(frames[f][..., 1], y)
+        assert np.all(frames[f][..., 2] == f)
