@@ -26,9 +26,10 @@ VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
 VAR_LDS6 = 6          # VAR_LDS built for >= 6 waves/SIMD (LDS copies that fit 6 but not 7 blocks per CU)
 VAR_LDS_POOL = 7      # LDS-resident scene, block-pooled shadow queries (trace_kernel_pool)
 VAR_LDS_POOL6 = 8     # VAR_LDS_POOL built for >= 6 waves/SIMD
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6)
-VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6)
-VAR_LAST = 8
+VAR_LDS_POOL1B = 9    # VAR_LDS_POOL with one block barrier per iteration (trace_kernel_pool1b)
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_POOL1B)
+VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_POOL1B)
+VAR_LAST = 9
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 

@@ -9,3 +9,9 @@ timeout -k 10 400 python tools/ab_builds.py --libs abtmp/libprt_qn64.so abtmp/li
 cat $O/ab_c4.jsonl
 timeout -k 10 200 python bench.py --config 4 --no-cpu-baseline > $O/bench_c4.json 2> $O/bench_c4.err
 tail -c 400 $O/bench_c4.json
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "variants or full_size or mis" > $O/pytest_var9.log 2>&1
+tail -2 $O/pytest_var9.log
+timeout -k 10 300 python tools/ab_variants.py --res 512 --spp 64 --depth 8 --rounds 5 --variants 7 9 > $O/ab_var79_c2.jsonl 2> $O/ab_var79_c2.err
+cat $O/ab_var79_c2.jsonl
+timeout -k 10 300 python tools/ab_variants.py --scene specular --res 1024 --spp 32 --depth 8 --rounds 3 --variants 7 9 > $O/ab_var79_c3.jsonl 2> $O/ab_var79_c3.err
+cat $O/ab_var79_c3.jsonl
