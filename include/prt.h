@@ -29,8 +29,8 @@ extern "C" {
 #endif
 
 /* ABI 2 (this build): prt_trace_rays, prt_hit_all added; trace-kernel variant ids renumbered
- * to 1..9 (PRT_FLAG_VARIANT; 7 / 8 / 9 are the pooled-shadow kernel; ids above 9 are rejected with
- * PRT_ERR_ARG, and ABI 1's ids 1..9 named other kernels, so a caller built against ABI 1 must
+ * to 1..8 (PRT_FLAG_VARIANT; 7 / 8 are the pooled-shadow kernel; ids above 8 are rejected with
+ * PRT_ERR_ARG, and ABI 1's ids 1..8 named other kernels, so a caller built against ABI 1 must
  * check prt_abi_version());
  * prt_scene_info's info8[4] is the BVH4 LDS traversal stack depth (0: BVH4 too deep for
  * the LDS-stack variants); watchdog flags are cleared once reported (prt_check_faults). */
@@ -60,7 +60,7 @@ extern "C" {
  * SIMD), 2 the same without an occupancy target, 3 global scene (quantised nodes, spill
  * stack), 4 / 5 the MIS estimator on an LDS / global scene, 6 the LDS-resident scene built
  * for >= 6 waves per SIMD, 7 / 8 the LDS-resident block-pooled shadow kernel for >= 7 / >= 6
- * waves per SIMD, 9 the pooled kernel with one block barrier per iteration).  Variants of one estimator produce
+ * waves per SIMD).  Variants of one estimator produce
  * bit-identical images; the selector exists for A/B runs and tests. */
 #define PRT_FLAG_VARIANT_SHIFT 8
 #define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFFu) << PRT_FLAG_VARIANT_SHIFT)
@@ -91,10 +91,6 @@ int prt_bvh_build(const float* tri_v, int64_t n_tri, int32_t max_leaf, void** ou
 int prt_bvh_info(void* bvh, int64_t* info6);
 /* nodes: n_nodes x 16 f32; tris: n_tri x 12 f32 (BVH order); order: n_tri (BVH slot -> triangle) */
 int prt_bvh_export(void* bvh, float* nodes, float* tris, int32_t* order);
-/* The compact BVH4 records the global-scene kernels traverse (one array of 48-B node and
- * triangle records, 12 f32 each, layout in pyrenderer_amd/csrc/prt_internal.h compact_bvh4):
- * *n_records is set; the records are copied to out when cap_records >= *n_records.  For tests. */
-int prt_bvh_compact(void* bvh, float* out, int64_t cap_records, int64_t* n_records);
 void prt_bvh_destroy(void* bvh);
 
 /* -------------------------------------------------------------- scene ----

@@ -26,10 +26,9 @@ VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
 VAR_LDS6 = 6          # VAR_LDS built for >= 6 waves/SIMD (LDS copies that fit 6 but not 7 blocks per CU)
 VAR_LDS_POOL = 7      # LDS-resident scene, block-pooled shadow queries (trace_kernel_pool)
 VAR_LDS_POOL6 = 8     # VAR_LDS_POOL built for >= 6 waves/SIMD
-VAR_LDS_POOL1B = 9    # VAR_LDS_POOL with one block barrier per iteration (trace_kernel_pool1b)
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_POOL1B)
-VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_POOL1B)
-VAR_LAST = 9
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6)
+VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6)
+VAR_LAST = 8
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 
@@ -56,7 +55,6 @@ EXPORTS = {
     "prt_bvh_build": (_i, [_vp, _i64, _i32, _vp]),
     "prt_bvh_info": (_i, [_vp, _vp]),
     "prt_bvh_export": (_i, [_vp, _vp, _vp, _vp]),
-    "prt_bvh_compact": (_i, [_vp, _vp, _i64, _vp]),
     "prt_bvh_destroy": (None, [_vp]),
     "prt_scene_create": (_i, [_i, _vp, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _i32, _vp, _vp]),
     "prt_scene_info": (_i, [_vp, _vp]),
@@ -143,14 +141,6 @@ class Bvh:
         order = np.zeros(self.n_tri, np.int32)
         check(lib().prt_bvh_export(self.h, ptr(nodes), ptr(tris), ptr(order)))
         return nodes, tris, order
-
-    def compact(self):
-        """The compact BVH4 records of the global-scene kernels: (n_records, 12) float32."""
-        n = ctypes.c_int64(0)
-        check(lib().prt_bvh_compact(self.h, None, 0, ctypes.byref(n)))
-        out = np.zeros((n.value, 12), np.float32)
-        check(lib().prt_bvh_compact(self.h, ptr(out), n.value, ctypes.byref(n)))
-        return out
 
     def __del__(self):
         if getattr(self, "h", None):

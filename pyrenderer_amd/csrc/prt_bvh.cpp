@@ -687,102 +687,4 @@ void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out) {
 }
 
 
-bool compact_bvh4(const Bvh4Host& b4, const BvhHost& b2, std::vector<float>* out, std::string* err) {
-    const double margin = 2.0 * (double)b2.pad;
-    out->clear();
-    if (b4.n_nodes == 0) return true;
-    // records: node records and triangle records, 12 floats each; the root is record 0
-    std::vector<float>& rec = *out;
-    auto alloc = [&](int64_t n) {
-        const int64_t r = (int64_t)rec.size() / 12;
-        rec.resize(rec.size() + (size_t)n * 12, 0.0f);
-        return r;
-    };
-    alloc(1);
-    // depth-first over the BVH4: (node, its record)
-    std::vector<std::pair<int64_t, int64_t>> todo{{0, 0}};
-    while (!todo.empty()) {
-        const int64_t n = todo.back().first, r = todo.back().second;
-        todo.pop_back();
-        const float* f = b4.nodes.data() + (size_t)n * 32;
-        int32_t refs[4];
-        std::memcpy(refs, f + 24, 16);
-        bool ok[4];
-        for (int k = 0; k < 4; ++k) ok[k] = std::isfinite(f[k]) && refs[k] != 0x7FFFFFFF;
-        // child block: inner children's node records, then the leaf children's triangles
-        int n_inner = 0;
-        for (int k = 0; k < 4; ++k) n_inner += (ok[k] && refs[k] >= 0) ? 1 : 0;
-        const int64_t base = alloc(n_inner);
-        uint32_t meta = 0, flags = 0;
-        int rank = 0, leaf_off = n_inner;
-        std::vector<std::pair<int64_t, int64_t>> kids;
-        for (int k = 0; k < 4; ++k) {
-            if (!ok[k]) { flags |= 16u << k; continue; }
-            if (refs[k] >= 0) {
-                flags |= 1u << k;
-                meta |= (uint32_t)rank << (8 * k);
-                kids.push_back({refs[k], base + rank});
-                ++rank;
-            } else {
-                const int32_t v = -refs[k] - 1;
-                const int64_t first = v >> 3;
-                const int cnt = (v & 7) + 1;
-                const int64_t t0 = alloc(cnt);
-                if (t0 != base + leaf_off) { *err = "compact BVH4: leaf block out of order"; return false; }
-                std::memcpy(rec.data() + (size_t)t0 * 12, b2.tris.data() + (size_t)first * 12, sizeof(float) * 12 * cnt);
-                meta |= (uint32_t)((leaf_off << 3) | (cnt - 1)) << (8 * k);
-                leaf_off += cnt;
-            }
-        }
-        if (leaf_off > 31) { *err = "compact BVH4: child block offset above 31"; return false; }
-        // quantisation: origin rounded down, grid step = the power of two at or above range / 254
-        float origin[3];
-        uint32_t ql[3] = {0, 0, 0}, qh[3] = {0, 0, 0}, ex[3] = {0, 0, 0};
-        for (int a = 0; a < 3; ++a) {
-            double lo = INFINITY, hi = -INFINITY;
-            for (int k = 0; k < 4; ++k)
-                if (ok[k]) {
-                    lo = std::min(lo, (double)f[(2 * a) * 4 + k]);
-                    hi = std::max(hi, (double)f[(2 * a + 1) * 4 + k]);
-                }
-            if (!(lo <= hi)) { lo = 0.0; hi = 0.0; }
-            float o = (float)(lo - margin);
-            if ((double)o > lo - margin) o = std::nextafter(o, -INFINITY);
-            const double ext = hi + margin - (double)o;
-            int e = 0;
-            (void)std::frexp(std::max(ext / 254.0, 1e-37), &e);   // 2^e >= ext / 254 > 2^(e-1)
-            e = std::max(-126, std::min(127, e));
-            const double st = std::ldexp(1.0, e);
-            origin[a] = o;
-            ex[a] = (uint32_t)(e + 127);   // f32 exponent field of 2^e (normal range)
-            for (int k = 0; k < 4; ++k) {
-                if (!ok[k]) continue;
-                const double l = (double)f[(2 * a) * 4 + k], h = (double)f[(2 * a + 1) * 4 + k];
-                long ql_k = (long)std::floor((l - margin - (double)o) / st);
-                long qh_k = (long)std::ceil((h + margin - (double)o) / st);
-                ql_k = std::max(0L, std::min(255L, ql_k));
-                qh_k = std::max(0L, std::min(255L, qh_k));
-                ql[a] |= (uint32_t)ql_k << (8 * k);
-                qh[a] |= (uint32_t)qh_k << (8 * k);
-            }
-        }
-        float* q = rec.data() + (size_t)r * 12;
-        const uint32_t b32 = (uint32_t)base;
-        const uint32_t exps = ex[0] | (ex[1] << 8) | (ex[2] << 16) | (flags << 24);
-        q[0] = origin[0]; q[1] = origin[1]; q[2] = origin[2]; std::memcpy(q + 3, &b32, 4);
-        std::memcpy(q + 4, &ql[0], 4); std::memcpy(q + 5, &qh[0], 4);
-        std::memcpy(q + 6, &ql[1], 4); std::memcpy(q + 7, &qh[1], 4);
-        std::memcpy(q + 8, &ql[2], 4); std::memcpy(q + 9, &qh[2], 4);
-        std::memcpy(q + 10, &exps, 4); std::memcpy(q + 11, &meta, 4);
-        // children in reverse so that the first inner child's subtree follows its block
-        for (auto it = kids.rbegin(); it != kids.rend(); ++it) todo.push_back(*it);
-    }
-    const int64_t n_rec = (int64_t)rec.size() / 12;
-    if (n_rec * 48 > (int64_t)UINT32_MAX || n_rec >= ((int64_t)1 << 28)) {
-        *err = "compact BVH4: more than 2^28 records or 4 GiB (32-bit record offsets)";
-        return false;
-    }
-    return true;
-}
-
 }  // namespace prt

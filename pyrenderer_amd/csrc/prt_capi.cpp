@@ -347,9 +347,6 @@ int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, int64_t n_items, prt::T
     if (prt::variant_quantized(var)) {
         P.nodes = (const float4*)s->nodes4q.p;
         P.n_node_f4 = (int)s->n_node4q_f4;
-#ifndef PRT_QN64
-        P.tris = (const float4*)s->nodes4q.p;   // compact records: triangles in the nodes' child blocks
-#endif
     }
     if (prt::variant_uses_lds(var) && !lds_fits4(s)) return fail(PRT_ERR_ARG, "scene too large for the LDS variant");
     if (prt::variant_pool(var) && (s->need4 > 32 || s->need4 < 1))
@@ -654,23 +651,6 @@ int prt_bvh_export(void* bvh, float* nodes, float* tris, int32_t* order) {
     return PRT_OK;
 }
 
-int prt_bvh_compact(void* bvh, float* out, int64_t cap_records, int64_t* n_records) {
-    auto* b = (prt::BvhHost*)bvh;
-    if (!b || !n_records) return fail(PRT_ERR_ARG, "NULL argument");
-    std::vector<float> rec;
-    std::string err;
-    try {
-        prt::Bvh4Host b4;
-        prt::collapse_bvh4(*b, &b4);
-        if (!prt::compact_bvh4(b4, *b, &rec, &err)) return fail(PRT_ERR_ARG, err);
-    } catch (const std::bad_alloc&) {
-        return fail(PRT_ERR_OOM, "host allocation failed");
-    }
-    *n_records = (int64_t)rec.size() / 12;
-    if (out && cap_records >= *n_records) std::memcpy(out, rec.data(), sizeof(float) * rec.size());
-    return PRT_OK;
-}
-
 void prt_bvh_destroy(void* bvh) { delete (prt::BvhHost*)bvh; }
 
 int prt_scene_create(int device, const float* tri_v, const float* tri_n, const int32_t* tri_mat, int64_t n_tri,
@@ -755,12 +735,7 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
             s->need4 = b4.stack_need;
             if ((rc = upload(s->nodes4, b4.nodes.data(), sizeof(float) * b4.nodes.size(), &s->device_bytes))) break;
             std::vector<float> q4;
-#ifdef PRT_QN64
             prt::quantize_bvh4(b4, bvh.pad, &q4);
-#else
-            // one array of 48-B node and triangle records (the quantised variants read both from it)
-            if (!prt::compact_bvh4(b4, bvh, &q4, &err)) { rc = fail(PRT_ERR_ARG, err); break; }
-#endif
             s->n_node4q_f4 = (int64_t)q4.size() / 4;
             if ((rc = upload(s->nodes4q, q4.data(), sizeof(float) * q4.size(), &s->device_bytes))) break;
         }
@@ -838,9 +813,6 @@ int prt_closest_hits(void* scene, const float* rays, int64_t n, uint32_t flags, 
     std::memset(&P, 0, sizeof(P));
     P.nodes = (const float4*)(quant ? s->nodes4q.p : s->nodes4.p);
     P.tris = (const float4*)s->tris.p;
-#ifndef PRT_QN64
-    if (quant) P.tris = (const float4*)s->nodes4q.p;   // compact records (prt_internal.h)
-#endif
     P.n_tri = (int)s->n_tri;
     P.n_sph = (int)s->n_sph;
     P.sph = (const float4*)s->sph.p;
@@ -872,9 +844,6 @@ int prt_hit_all(void* scene, const float* rays, int64_t n, uint64_t seed, uint32
     prt::TraceParams P;
     scene_params(s, P);
     if (quant) P.nodes = (const float4*)s->nodes4q.p;
-#ifndef PRT_QN64
-    if (quant) P.tris = (const float4*)s->nodes4q.p;
-#endif
     P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
     P.fault = (int*)((char*)s->work.p + kFaultOffset);
     DevBuf d_rays, d_id, d_t, d_out;

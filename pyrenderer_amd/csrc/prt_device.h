@@ -471,7 +471,6 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     bool h0, h1, h2, h3;
     int r0, r1, r2, r3;
     if (QN) {
-#ifdef PRT_QN64
         // 64-B nodes at a 32-bit byte offset from the uniform base (saddr + voffset addressing,
         // no 64-bit address arithmetic): BVH4 nodes < refs / 3 < 2^25, so the offset < 2^31
         const float4* nd = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + ((uint32_t)cur << 6));
@@ -488,37 +487,6 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
         h1 = qchild(1, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t1) && r1 != kSentinel;
         h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && r2 != kSentinel;
         h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && r3 != kSentinel;
-#else
-        // compact 48-B records (prt_internal.h compact_bvh4) at a 32-bit byte offset from the
-        // uniform base: three 16-B loads per lane instead of four — the global-scene traversal is
-        // bound by the vector L1's tag lookups (one per distinct line per wave load instruction:
-        // TA / TD busy 0.92 / 0.98 of the C4 launch, profiles/r04/pmc_mem/)
-        const float4* nd = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint32_t)cur * 48u);
-        const float4 a = nd[0], b = nd[1], c = nd[2];
-        if (STATS) { cn.nodes++; cn.it_inner++; }
-        const uint32_t ex = __float_as_uint(c.z), meta = __float_as_uint(c.w), base = __float_as_uint(a.w);
-        // grid steps 2^e from the f32 exponent fields (exact), applied to 1/d like quantize_bvh4's steps
-        const float s_x = __uint_as_float((ex & 0xFFu) << 23), s_y = __uint_as_float(((ex >> 8) & 0xFFu) << 23);
-        const float s_z = __uint_as_float(((ex >> 16) & 0xFFu) << 23);
-        QAxis X = {s_x * inv.x, __builtin_fmaf(a.x, inv.x, -oi.x)};
-        QAxis Y = {s_y * inv.y, __builtin_fmaf(a.y, inv.y, -oi.y)};
-        QAxis Z = {s_z * inv.z, __builtin_fmaf(a.z, inv.z, -oi.z)};
-        uint32_t lxq = __float_as_uint(sx ? b.y : b.x), hxq = __float_as_uint(sx ? b.x : b.y);
-        uint32_t lyq = __float_as_uint(sy ? b.w : b.z), hyq = __float_as_uint(sy ? b.z : b.w);
-        uint32_t lzq = __float_as_uint(sz ? c.y : c.x), hzq = __float_as_uint(sz ? c.x : c.y);
-        // child refs without a load: inner = base + rank, leaf = ~((base << 3) + ((offset << 3) | (count - 1)))
-        const uint32_t fl = ex >> 24;
-        const uint32_t b8 = base << 3;
-        auto ref = [&](int k) {
-            const uint32_t off = (meta >> (8 * k)) & 0xFFu;
-            return (fl >> k) & 1u ? (int)(base + off) : (int)~(b8 + off);
-        };
-        r0 = ref(0); r1 = ref(1); r2 = ref(2); r3 = ref(3);
-        h0 = qchild(0, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t0) && !(fl & 16u);
-        h1 = qchild(1, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t1) && !(fl & 32u);
-        h2 = qchild(2, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t2) && !(fl & 64u);
-        h3 = qchild(3, lxq, hxq, lyq, hyq, lzq, hzq, X, Y, Z, tmin, best, t3) && !(fl & 128u);
-#endif
     } else {
         float4 nx, fx, ny, fy, nz, fz, rf;
         if (OCT) {
@@ -641,27 +609,6 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 while (mc > 1 && !__ballot(cnt >= mc)) --mc;
                 if (__builtin_amdgcn_readfirstlane(__lane_id()) == __lane_id()) cn.w_tri += mc;
             }
-#ifdef PRT_TRI_PIPE
-            if constexpr (QN) {
-                // global scenes: the next triangle's record is loaded while this one is tested (one
-                // L2 round trip per leaf instead of one per triangle); the last trip reloads its own
-                const float4* tp = tris + (size_t)first * 3;
-                float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
-                for (int k = 0; k < cnt; ++k) {
-                    const float4* tn = tp + 3 * min(k + 1, cnt - 1);
-                    const float4 n0 = tn[0], n1 = tn[1], n2 = tn[2];
-                    int id = __float_as_int(q0.w);
-                    float t;
-                    if (STATS) cn.tris++;
-                    if (mt_u(xyz(q0), xyz(q1), xyz(q2), o, d, tmin, best, id, best_id, any, t)) {
-                        best = t;
-                        best_id = id;
-                        if (any) { cur = S::kSent; break; }
-                    }
-                    q0 = n0; q1 = n1; q2 = n2;
-                }
-            } else
-#endif
             for (int k = 0; k < cnt; ++k) {
                 const float4* tp = tris + (size_t)(first + k) * 3;
                 float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
@@ -1506,421 +1453,17 @@ constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 
 #define PRT_POOL_S_PRIO 2
 #endif
 
+// One block barrier per iteration (round 4; round 3's kernel had two: after E and after S, with
+// the answers resolved in between).  A lane's S answer is resolved in the NEXT iteration, after
+// its next extension traversal (which does not depend on it) and before it shades that hit, so
+// the reference's order of additions holds and images stay bit-identical.  A wave with a pending
+// shadow ray waits only until the previous S phase's chunks are answered (an LDS counter, normally
+// done by then); S waves run beside the other waves' next traversals, and waves without a chunk go
+// straight on to their refill (C2 4.049 vs 4.080 ms, C3 at 1024^2 x 32 spp 9.455 vs 9.570 ms per
+// launch against the two-barrier kernel, profiles/r04/pool1b/).
 template <bool STATS, int WPE>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel_pool(TraceParams P) {
-    extern __shared__ float4 smem[];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int stack_f4 = P.lds_stack * kBlock * 2 / 16;
-    LdsStack16 stk;
-    stk.l = reinterpret_cast<short*>(smem) + (tid & ~63) + 2 * (tid & 31) + ((tid >> 5) & 1);
-    float* pool = reinterpret_cast<float*>(smem + stack_f4);   // [7][256]
-    uint8_t* queue = reinterpret_cast<uint8_t*>(smem + stack_f4 + kPoolF4);
-    uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + stack_f4 + kPoolF4 + kQueueF4);
-    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + kCtlF4;
-    const int n_node4 = P.n_node_f4 / 8;
-    float4* st4 = sn + 56 * n_node4;
-    float4* slv = st4 + P.n_tri_f4;
-    int* slo = reinterpret_cast<int*>(slv + 4 * P.n_lt);
-    float4* smt = slv + 4 * P.n_lt + (P.n_light + 4) / 4;   // materials, after the light offsets
-    copy_octant_nodes(sn, P.nodes, n_node4);
-    for (int i = tid; i < P.n_tri_f4; i += kBlock) st4[i] = P.tris[i];
-    for (int i = tid; i < 4 * P.n_lt; i += kBlock) slv[i] = P.light_v[i];
-    for (int i = tid; i <= P.n_light; i += kBlock) slo[i] = P.light_off[i];
-    for (int i = tid; i < 2 * P.n_mat; i += kBlock) smt[i] = reinterpret_cast<const float4*>(P.mats)[i];
-    if (tid < 6) ctl[tid] = 0u;
-    __syncthreads();
-    const float4* g_nodes = sn;
-    const float4* g_tris = st4;
-    // normals and shading frames come from global memory (L1-resident): with either the LDS copy
-    // no longer fits seven blocks per CU at config 2; the materials sit in LDS (C2 -1.3 %, C3
-    // -1.8 % against global loads, profiles/r03/s9/)
-    const float4* s_nm = P.tri_nm;
-    const float4* s_fr = P.tri_frame;
-    const float* s_mats = reinterpret_cast<const float*>(smt);
-
-    uint32_t q_next = 0, q_end = 0;
-    bool exhausted = false;
-    int item = -1;
-    int bounce = 0;
-    bool my_sh = false;      // this lane waits for the result of its pooled shadow ray
-    uint32_t st = 0;
-    V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
-    V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
-    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t n_e = 0, n_s = 0, lanes_s = 0, pre_hits = 0;
-    uint32_t chunk_s = 0, chunk_xy0 = 0;
-    int parity = 0;
-#ifdef PRT_POOL_CLOCKS
-    // diagnostic build (tools/pool_clocks.py): wave-level cycles in E, at barrier 1, in S, at barrier 2
-    uint64_t ck[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t t_c = __builtin_amdgcn_s_memtime();
-#define PRT_CLOCK(k) do { const uint64_t t_n = __builtin_amdgcn_s_memtime(); ck[k] += t_n - t_c; t_c = t_n; } while (0)
-#else
-#define PRT_CLOCK(k) do {} while (0)
-#endif
-    // work-queue refill of the wave's idle lanes (path regeneration, trace_kernel's refill)
-    auto refill = [&]() {
-            bool me_idle = item < 0;
-            uint64_t idle = __ballot(me_idle);
-            for (int round = 0; round < 2 && idle; ++round) {
-                uint32_t avail = q_end - q_next;
-                if (avail == 0 && !exhausted) {
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(P.work, (uint32_t)kChunk);
-                    base = __builtin_amdgcn_readfirstlane(base);
-                    if ((uint64_t)base >= P.n_items) {
-                        exhausted = true;
-                    } else {
-                        q_next = base;
-                        q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
-                        chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
-                        uint32_t tk = (base - chunk_s * (uint32_t)P.n_slots) >> P.log_tpx;
-                        chunk_xy0 = ((const __attribute__((address_space(4))) uint32_t*)(uintptr_t)P.tile_xy)[tk];
-                    }
-                    avail = q_end - q_next;
-                }
-                if (avail == 0) break;
-                uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                uint32_t need = (uint32_t)__popcll(idle);
-                uint32_t take = need < avail ? need : avail;
-                if (me_idle && rank < take) {
-                    item = (int)(q_next + rank);
-                    L = v3(0, 0, 0);
-                    int x, y;
-                    pixel_of(P, (uint32_t)item, chunk_s, chunk_xy0, x, y);
-                    int W = P.W, H = P.H;
-                    asm volatile("" : "+s"(W), "+s"(H));
-                    bool ok = x < W && y < H;
-                    if (ok) {
-                        if (P.rays) {
-                            float4 r = P.rays[item];
-                            d = v3(r.x, r.y, r.z);
-                            st = __float_as_uint(r.w);
-                            if (P.ray_o) {
-                                const float4 ro = P.ray_o[item];
-                                o = v3(ro.x, ro.y, ro.z);
-                            } else {
-                                float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
-                                asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
-                                o = v3(o0, o1, o2);
-                            }
-                        } else {
-                            camera_ray(P, x, y, chunk_s, st, o, d);
-                        }
-                    }
-                    if (!ok) {
-                        float* out = P.out + (size_t)item * 3;
-                        out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
-                        item = -2;
-                    } else {
-                        beta = v3(1, 1, 1);
-                        bounce = 0;
-                        // the primary ray as this lane's next ray (R takes o from the pool, d from wi)
-                        pool[0 * kBlock + tid] = o.x; pool[1 * kBlock + tid] = o.y; pool[2 * kBlock + tid] = o.z;
-                        wi = d;
-                    }
-                }
-                q_next += take;
-                me_idle = item == -1;
-                idle = __ballot(me_idle);
-            }
-        if (item == -2) item = -1;
-    };
-    while (true) {
-        // ------------------------------------------------------------------ E phase
-        refill();
-        PRT_CLOCK(4);
-        if (__ballot(item >= 0) != 0) {
-            if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_e++;
-            if (item >= 0) {
-                int hid = -1;
-                float ht = 0.0f;
-                if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
-                bool hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
-                    g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
-                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
-                if (P.n_sph > 0) {
-                    float best = hit ? ht : kTMax;
-                    for (int k = 0; k < P.n_sph; ++k) {
-                        float root;
-                        if (sphere_hit(P.sph[k], o, d, kTMin, best, root)) {
-                            best = root;
-                            hid = P.n_tri + k;
-                            hit = true;
-                        }
-                    }
-                    ht = best;
-                }
-                PRT_CLOCK(5);
-                bool finished = false;
-                if (!hit) {
-                    finished = true;
-                } else {
-                    V3 p = o + d * ht;
-                    V3 ng;
-                    int mid;
-                    if (hid < P.n_tri) {
-                        float4 nm = s_nm[hid];
-                        ng = xyz(nm);
-                        mid = __float_as_int(nm.w);
-                    } else {
-                        asm volatile("");
-                        float4 sc = P.sph[hid - P.n_tri];
-                        ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
-                        mid = P.sph_mat[hid - P.n_tri];
-                    }
-                    const float* m = s_mats + 8 * mid;
-                    const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;
-                    const V3 n = flip ? neg(ng) : ng;
-                    if (m[5] == 2.0f || m[5] == 3.0f) {
-                        bool front = dot(d, ng) < 0.0f;
-                        V3 ns = front ? ng : neg(ng);
-                        V3 unit = normalize(d);
-                        V3 out;
-                        bool absorbed = false;
-                        if (m[5] == 2.0f) {
-                            out = reflect3(unit, ns);
-                            if (m[7] > 0.0f) out = out + random_in_unit_sphere(st) * m[7];
-                            absorbed = !(dot(out, ns) > 0.0f);
-                        } else {
-                            float ratio = front ? 1.0f / m[6] : m[6];
-                            float ct = -dot(unit, ns);
-                            ct = ct > 1.0f ? 1.0f : ct;
-                            float stn = sqrtf(1.0f - ct * ct);
-                            bool cannot = ratio * stn > 1.0f;
-                            if (cannot || schlick(ct, ratio) > rng_next(st)) out = reflect3(unit, ns);
-                            else out = refract3(unit, ns, ratio);
-                        }
-                        if (absorbed) {
-                            finished = true;
-                        } else {
-                            beta = beta * v3(m[0], m[1], m[2]);
-                            wi = normalize(out);   // next ray (p, wi), taken up in R
-                            ++bounce;
-                            if (bounce >= P.depth) finished = true;
-                        }
-                    } else if (m[3] != 0.0f) {
-                        float d1 = dot(neg(d), n);
-                        if (d1 > 0.0f) {
-                            V3 lc = v3(P.dl_r, P.dl_g, P.dl_b);
-                            L = bounce == 0 ? L + lc * beta : L + (lc * beta) * d1;
-                        }
-                        finished = true;
-                    } else {
-                        float u0 = rng_next(st);
-                        float u1 = rng_next(st);
-                        V3 l = cosine_hemisphere<true>(u0, u1);
-                        const float4* fr = s_fr + ((size_t)(hid < P.n_tri ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
-                        if (hid < P.n_tri) {
-                            float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
-                            wi = normalize<true>(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
-                        } else {
-                            wi = to_world(n, l);
-                        }
-                        float pdf = fabsf(dot(n, wi)) * kInvPi;
-                        V3 att = v3(m[0], m[1], m[2]);
-                        float cw = dot(n, wi);
-                        float dz = cw > 0.0f ? cw : 0.0f;
-                        V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                        V3 adp = div3_nan_guard(ad, pdf);
-                        V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
-                        beta = beta * nb;
-                        int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
-                        int lo = slo[li];
-                        int f = rng_int(st, 0, slo[li + 1] - lo - 1);
-                        float su = sqrt_cr<true>(rng_next(st));
-                        float sv = rng_next(st);
-                        float a = su * (1.0f - sv);
-                        float b = su * sv;
-                        const float4* lv = slv + (size_t)(lo + f) * 4;
-                        float4 L0 = lv[0], L1 = lv[1], L2 = lv[2], LN = lv[3];
-                        float c = 1.0f - a - b;
-                        V3 p2 = (xyz(L0) * a + xyz(L1) * b) + xyz(L2) * c;
-                        V3 n2 = xyz(LN);
-                        V3 w = normalize<true>(p2 - p);
-                        float t_at = (p2.x - p.x) / w.x;
-                        float dot1 = dot(n, w), dot2 = -dot(n2, w);
-                        bool queued = false;
-                        if (dot1 > 0.0f && dot2 > 0.0f) {
-                            if (STATS) cn.shadow++;
-                            // the sampled light triangle itself, in the traversal's arithmetic: a hit
-                            // in (t_min, t_at_light) answers the any-hit query (occluded)
-                            float tl;
-                            const V3 lv0 = xyz(L0);
-                            const bool self_hit = mt_u(lv0, xyz(L1) - lv0, xyz(L2) - lv0, p, w, kTMin, t_at, 0, -1,
-                                                       true, tl);
-                            if (STATS) { cn.tris++; pre_hits += self_hit ? 1 : 0; }
-                            if (!self_hit) {
-                                const float* em = s_mats + 8 * __float_as_int(LN.w);
-                                V3 dd = p - p2;
-                                float sl = dot(dd, dd);
-                                V3 rad = div3(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl);
-                                pend = beta * rad;
-                                pool[3 * kBlock + tid] = w.x; pool[4 * kBlock + tid] = w.y; pool[5 * kBlock + tid] = w.z;
-                                pool[6 * kBlock + tid] = t_at;
-                                queued = true;
-                            }
-                        }
-                        if (queued) {
-                            my_sh = true;
-                        } else {
-                            ++bounce;
-                            if (bounce >= P.depth) finished = true;
-                        }
-                    }
-                    // every continuing lane parks its next ray's origin p in its pool slot (the
-                    // shadow ray's origin too) and its direction in wi: neither stays live in
-                    // registers across the S phase, where the lane may traverse another lane's ray
-                    pool[0 * kBlock + tid] = p.x; pool[1 * kBlock + tid] = p.y; pool[2 * kBlock + tid] = p.z;
-                }
-                if (finished) {
-                    float* out = P.out + (size_t)item * 3;
-                    out[0] = L.x; out[1] = L.y; out[2] = L.z;
-                    if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
-                    item = -1;
-                }
-            }
-        }
-        // enqueue this wave's shadow rays: one LDS atomic per wave, thread ids at the ranks
-        {
-            const uint64_t m = __ballot(my_sh);
-            const uint32_t cnt = (uint32_t)__popcll(m);
-            uint32_t base = 0;
-            if (cnt) {
-                if (lane == __builtin_amdgcn_readfirstlane(lane)) base = atomicAdd(&ctl[parity], cnt);
-                base = __builtin_amdgcn_readfirstlane(base);
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                if (my_sh) queue[base + rank] = (uint8_t)tid;
-            }
-            // a wave with busy lanes or unclaimed work keeps the block looping
-            if ((__ballot(item >= 0) != 0 || !exhausted) && lane == 0) ctl[2 + parity] = 1u;
-        }
-        PRT_CLOCK(0);
-        __syncthreads();
-        PRT_CLOCK(1);
-        // ------------------------------------------------------------------ S phase
-        const uint32_t n_q = ctl[parity];
-        if (tid == 0) { ctl[parity ^ 1] = 0u; ctl[2 + (parity ^ 1)] = 0u; ctl[4 + (parity ^ 1)] = 0u; }
-        // the queue's rays in ceil(n / 64) chunks, one to each of the first waves to claim one (<= 4
-        // chunks, one claim per wave); the others refill the lanes that finished in E meanwhile,
-        // off the critical path
-        const uint32_t n_chunks = (n_q + 63u) >> 6;
-        uint32_t chunk = 0xFFFFFFFFu;
-        if (n_chunks) {
-            if (lane == 0) chunk = atomicAdd(&ctl[4 + parity], 1u);
-            chunk = __builtin_amdgcn_readfirstlane(chunk);
-        }
-        if (chunk >= n_chunks) refill();
-        if (chunk < n_chunks) {
-            // the S waves hold up their whole block at barrier 2: issue priority over other blocks
-            __builtin_amdgcn_s_setprio(PRT_POOL_S_PRIO);
-            // full 64-ray chunks and one partial (equal-size chunks: C2 +0.5 %, C3 +0.8 %; the
-            // arrival-ordered claim with an early refill by the first two waves at barrier 1: C2
-            // +1.2 %, C3 +0.9 %; profiles/r03/pool/)
-            const uint32_t e0 = chunk * 64u, e1 = min(n_q, e0 + 64u);
-            const uint32_t e = e0 + (uint32_t)lane;
-            if (STATS && lane == 0) { n_s++; lanes_s += e1 - e0; }
-            if (e < e1) {
-                const int owner = queue[e];
-                const V3 so = v3(pool[0 * kBlock + owner], pool[1 * kBlock + owner], pool[2 * kBlock + owner]);
-                const V3 sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
-                const float stm = pool[6 * kBlock + owner];
-                int hid = -1;
-                float ht = 0.0f;
-                if (STATS) cn.q0 = cn.nodes;
-                bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
-                    g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
-                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
-                if (P.n_sph > 0 && !hit) {
-                    for (int k = 0; k < P.n_sph; ++k) {
-                        float root;
-                        if (sphere_hit(P.sph[k], so, sd, kTMin, stm, root)) { hit = true; break; }
-                    }
-                }
-                // the result travels back in the owner's t_max word: NaN = occluded
-                pool[6 * kBlock + owner] = hit ? __int_as_float(0x7FC00000) : 0.0f;
-            }
-            __builtin_amdgcn_s_setprio(0);
-        }
-        PRT_CLOCK(2);
-        __syncthreads();
-        PRT_CLOCK(3);
-        // ------------------------------------------------------------------ R: resolve
-        if (item >= 0) {
-            if (my_sh) {
-                const float r = pool[6 * kBlock + tid];
-                if (r == r) L = L + pend;   // not occluded
-                my_sh = false;
-                ++bounce;
-                if (bounce >= P.depth) {
-                    float* out = P.out + (size_t)item * 3;
-                    out[0] = L.x; out[1] = L.y; out[2] = L.z;
-                    if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
-                    item = -1;
-                }
-            }
-        }
-        // the next extension ray: origin from the pool slot, direction wi (assigned on every lane,
-        // idle ones included, so that no register keeps the previous ray across the S phase)
-        o = v3(pool[0 * kBlock + tid], pool[1 * kBlock + tid], pool[2 * kBlock + tid]);
-        d = wi;
-        const bool alive = ctl[2 + parity] != 0u;
-        parity ^= 1;
-        if (!alive) break;
-    }
-#ifdef PRT_POOL_CLOCKS
-    if (lane == 0)
-        for (int k = 0; k < 6; ++k) atomicAdd(P.stats + 24 + k, (unsigned long long)ck[k]);
-#endif
-#undef PRT_CLOCK
-    if (STATS) {
-        uint64_t a = cn.nodes, b = cn.tris, c = cn.ext, e = cn.shadow;
-        for (int off = 32; off > 0; off >>= 1) {
-            a += __shfl_down(a, off); b += __shfl_down(b, off);
-            c += __shfl_down(c, off); e += __shfl_down(e, off);
-        }
-        uint64_t ph[5] = {n_e, n_s, lanes_s, pre_hits, 0};
-        for (int k = 0; k < 4; ++k)
-            for (int off = 32; off > 0; off >>= 1) ph[k] += __shfl_down(ph[k], off);
-        if (lane == 0) {
-            atomicAdd(P.stats + 0, (unsigned long long)a);
-            atomicAdd(P.stats + 1, (unsigned long long)b);
-            atomicAdd(P.stats + 2, (unsigned long long)c);
-            atomicAdd(P.stats + 3, (unsigned long long)e);
-            // diag 17..20 (pool kernel): wave E iterations, wave S iterations, lanes of the S
-            // iterations, shadow rays answered by the light-triangle test
-            for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, (unsigned long long)ph[k]);
-        }
-        uint32_t msp = cn.max_sp, nf = cn.nonfinite, mq = cn.max_q;
-        for (int off = 32; off > 0; off >>= 1) {
-            msp = max(msp, (uint32_t)__shfl_down((int)msp, off));
-            nf += (uint32_t)__shfl_down((int)nf, off);
-            mq = max(mq, (uint32_t)__shfl_down((int)mq, off));
-        }
-        if (lane == 0) {
-            atomicMax(P.stats + 13, (unsigned long long)msp);
-            if (nf) atomicAdd(P.stats + 14, (unsigned long long)nf);
-            atomicMax(P.stats + 16, (unsigned long long)mq);
-        }
-    }
-}
-
-
-// One-barrier variant of trace_kernel_pool (variant 9): the same E / S phases, but the S phase's
-// answers are resolved in the NEXT iteration, after the lane's next extension traversal (which
-// does not depend on them) and before its shading, so the second block barrier goes: a wave
-// with a pending shadow ray waits only until the previous S phase's chunks are done (an LDS
-// counter, normally long done by then), S waves run beside the other waves' next traversals, and
-// the waves without a chunk go straight on to their refill.  Each lane still resolves its NEE
-// radiance before it shades its next hit (the reference's order of additions), so images are
-// bit-identical to variant 7's.
-template <bool STATS, int WPE>
-__global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
-void trace_kernel_pool1b(TraceParams P) {
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -2361,8 +1904,7 @@ void trace_kernel_pool1b(TraceParams P) {
     X(kVarLds6, 8, true, 6)                   \
     X(kVarGlobalMis, 480, false, 6)           \
     X(kVarLdsPool, 512, true, 7)              \
-    X(kVarLdsPool6, 512, true, 6)             \
-    X(kVarLdsPool1B, 1536, true, 7)
+    X(kVarLdsPool6, 512, true, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
@@ -2371,7 +1913,7 @@ static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStr
     if constexpr ((VAR & 512) != 0) {
         // the pool kernel's LDS stack size is a launch parameter (P.lds_stack): one instantiation,
         // compiled in its own unit (prt_trace_pool.hip, other register-allocation flags)
-        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, (VAR & 1024) != 0, grid, smem, stream);
+        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, grid, smem, stream);
         else return hipErrorInvalidValue;
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
         trace_kernel<STACK, STATS, VAR, LDS, WPE><<<grid, kBlock, smem, stream>>>(P);
@@ -2396,7 +1938,7 @@ template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
 static void occ_one(int* n, size_t smem) {
     constexpr bool spill = (VAR & 32) != 0;
     if constexpr ((VAR & 512) != 0) {
-        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, (VAR & 1024) != 0, smem);
+        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, smem);
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(n, trace_kernel<STACK, STATS, VAR, LDS, WPE>, kBlock, smem);
 }

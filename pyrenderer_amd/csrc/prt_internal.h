@@ -62,24 +62,6 @@ void collapse_bvh4(const BvhHost& b2, Bvh4Host* out);
 constexpr int kNodeQF4 = 4;
 void quantize_bvh4(const Bvh4Host& b4, float pad, std::vector<float>* out);
 
-// Compact quantised BVH4 for scenes read from HBM (round 4): ONE array of 48-B records holding
-// both the nodes and the triangle records (3 float4 each, the BVH2 triangle layout), so a node
-// visit loads 3 x 16 B per lane instead of 4 (global-scene traversal is bound by the CU's vector
-// L1 / address path: every wave load costs one tag lookup per distinct line its lanes touch).
-// A node's children live in one contiguous block at `base`: its inner children's node records
-// first (in slot order), then each leaf child's triangle records.  Node record:
-//   f[0] = (origin.x, origin.y, origin.z, bits(base))
-//   f[1] = (qlo.x[4], qhi.x[4], qlo.y[4], qhi.y[4])   u8 grid coordinates per child
-//   f[2] = (qlo.z[4], qhi.z[4], bits(exps), bits(meta))
-// exps: bytes 0..2 = the f32 exponent field of the grid step 2^e per axis (a power of two at
-// or above range / 254), byte 3 = inner-child mask (bits 0..3) | empty-slot mask (bits 4..7);
-// meta byte k = child k's offset from base (inner child: its rank among the inner children;
-// leaf: (record offset << 3) | (count - 1)).  Child refs therefore decode without a load:
-// inner = base + off, leaf = ~((base << 3) + off) (= leaf_ref(base + (off >> 3), (off & 7) + 1)).
-// Boxes are rounded outward with the same >= 2 pad of slack as quantize_bvh4 (conservative).
-constexpr int kCRecF4 = 3;
-// returns false (and *err) when the array would exceed the kernel's 32-bit byte offsets
-bool compact_bvh4(const Bvh4Host& b4, const BvhHost& b2, std::vector<float>* out, std::string* err);
 
 // Builds a binned-SAH BVH2 over triangles (tri_v: n x 9 f32 world vertices).
 // Box padding keeps the slab test conservative w.r.t. Moller-Trumbore's own

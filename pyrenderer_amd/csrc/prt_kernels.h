@@ -77,10 +77,8 @@ constexpr int kVarLds6 = 6;        // kVarLds built for >= 6 waves/SIMD (80 VGPR
 constexpr int kVarLdsPool = 7;     // LDS-resident scene, block-pooled shadow queries (trace_kernel_pool),
                                    // >= 7 waves/SIMD; the LDS stack size is P.lds_stack
 constexpr int kVarLdsPool6 = 8;    // kVarLdsPool built for >= 6 waves/SIMD (80 VGPRs)
-constexpr int kVarLdsPool1B = 9;   // trace_kernel_pool1b: the pooled kernel with one block barrier per
-                                   // iteration (answers resolved after the next extension traversal)
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 9;
+constexpr int kVarLast = 8;
 bool variant_pool(int var);
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
@@ -107,8 +105,7 @@ hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_sl
                           int y0, int w, int h, float* out, hipStream_t stream);
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 // the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
-hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, bool onebar, int grid, size_t smem,
-                             hipStream_t stream);
-int trace_occ_pool(bool stats, int wpe, bool onebar, size_t smem);
+hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream);
+int trace_occ_pool(bool stats, int wpe, size_t smem);
 
 }  // namespace prt

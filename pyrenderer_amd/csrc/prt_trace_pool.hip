@@ -10,13 +10,8 @@
 
 namespace prt {
 
-hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, bool onebar, int grid, size_t smem,
-                             hipStream_t stream) {
-    if (onebar) {
-        if (wpe != 7) return hipErrorInvalidValue;
-        if (stats) trace_kernel_pool1b<true, 7><<<grid, kBlock, smem, stream>>>(P);
-        else trace_kernel_pool1b<false, 7><<<grid, kBlock, smem, stream>>>(P);
-    } else if (stats) {
+hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream) {
+    if (stats) {
         if (wpe == 7) trace_kernel_pool<true, 7><<<grid, kBlock, smem, stream>>>(P);
         else if (wpe == 6) trace_kernel_pool<true, 6><<<grid, kBlock, smem, stream>>>(P);
         else return hipErrorInvalidValue;
@@ -28,13 +23,9 @@ hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, bool one
     return hipGetLastError();
 }
 
-int trace_occ_pool(bool stats, int wpe, bool onebar, size_t smem) {
+int trace_occ_pool(bool stats, int wpe, size_t smem) {
     int n = 0;
-    if (onebar) {
-        if (wpe != 7) return 0;
-        if (stats) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool1b<true, 7>, kBlock, smem);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool1b<false, 7>, kBlock, smem);
-    } else if (stats) {
+    if (stats) {
         if (wpe == 7) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<true, 7>, kBlock, smem);
         else if (wpe == 6) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<true, 6>, kBlock, smem);
     } else {
