@@ -1,7 +1,7 @@
 #!/bin/bash
 # After tools/round_full.sh <dir> ran on the GPU box: merge its PMC passes into profiles/pmc.json
 # and copy the rocprof summaries, counter CSVs, bench lines and test log into profiles/<dest>.
-#   bash tools/round_collect.sh gpurun_out/round profiles/r03/final
+#   bash tools/round_collect.sh gpurun_out/round profiles/r04/final
 set -e
 SRC=$1; DST=$2
 [ -d $SRC/prof_c2 ] && python tools/pmc_summary.py --dir $SRC/prof_c2 --key cornell_512x512x64spp_d8 > /dev/null
