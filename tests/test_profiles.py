@@ -46,3 +46,24 @@ def test_rocprof_summary_agrees_with_the_bench_events(key):
     rocprof_ms = float(rows[0]["AverageNs"]) / 1e6
     assert abs(rocprof_ms - line["roofline"]["kernel_avg_ms"]) <= 0.05 * rocprof_ms, (rocprof_ms, line["roofline"])
     assert line["roofline"]["kernel_sha"] == json.load(open(PMC))[key]["kernel_sha"]
+
+
+def test_no_roofline_fraction_above_one():
+    """Every committed bench line of this round prices its work against a resource it can actually
+    saturate: no `frac` field anywhere in the line exceeds 1 (round 3's `hbm_logical` priced LDS reads
+    against the HBM peak and read 1.06)."""
+    import glob
+
+    def fracs(o, path=""):
+        if isinstance(o, dict):
+            for k, v in o.items():
+                if k == "frac" and isinstance(v, (int, float)):
+                    yield path + "/" + k, v
+                yield from fracs(v, path + "/" + k)
+
+    files = sorted(glob.glob(os.path.join(FINAL, "bench_all", "c*.json")))
+    assert len(files) == 5
+    for f in files:
+        line = json.loads(open(f).read().strip().splitlines()[-1])
+        bad = [(p, v) for p, v in fracs(line) if not 0 <= v <= 1]
+        assert not bad, (f, bad)
