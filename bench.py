@@ -96,8 +96,8 @@ def parse():
     ap.add_argument("--scheme", default="latin", help="tile assignment: latin | mod")
     ap.add_argument("--frames-per-launch", type=int, default=0,
                     help="frames per render call (prt_render_frames_device: their items share the persistent "
-                         "launches, one ramp-up and drain per call); 0 = auto: min(steps, 16), 1 for frames of "
-                         "> 64 M samples per rank")
+                         "launches, one ramp-up and drain per call); 0 = auto: enough frames for >= ~16 M items "
+                         "per launch, 16..256, at most the steps; 1 for frames of > 64 M samples per rank")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N > 1: nccl (= RCCL over xGMI, the default) or gloo "
                          "(tile sums staged through host memory; rehearses the N > 1 path with several ranks "
@@ -326,7 +326,10 @@ def main():
     # per frame; each frame is still rendered, reduced, gathered and scattered whole
     F = args.frames_per_launch
     if F <= 0:
-        F = min(args.steps, 16) if rank_samples <= 64e6 else 1
+        # enough frames for a launch of >= ~16 M items (one C2 frame), at least 16 and at most 256:
+        # 16 for C2 on 1-8 GPUs, 256 for config 1's 65 k-sample frames; frames above 64 M samples
+        # (C3, C5) already fill their launches
+        F = min(256, max(16, -(-int(16.8e6) // max(int(rank_samples), 1)))) if rank_samples <= 64e6 else 1
     F = max(1, min(F, args.steps))
     n_streams = args.streams
     if n_streams <= 0:

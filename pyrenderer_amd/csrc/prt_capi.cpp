@@ -520,12 +520,12 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
             }
             P.wave_clock = nullptr;
         }
-        // per frame overlapping the chunk: its samples [a, b) of the launch sample space, in order
-        for (int64_t f = s0 / spp; f < n_frames && f * spp < s0 + n; ++f) {
-            const int64_t a = std::max<int64_t>(s0, f * spp), b = std::min<int64_t>(s0 + n, (f + 1) * spp);
-            HIP_TRY(prt::launch_reduce((const float*)cx->buf.p + (size_t)(a - s0) * n_slots * 3,
-                                       d_acc + (size_t)f * n_slots * 3, (int)n_slots, (int)(b - a),
-                                       a == f * spp && !accumulate, stream));
+        // every frame overlapping the chunk, one launch: frame f sums its samples of [s0, s0 + n) in order
+        {
+            const int64_t f0 = s0 / spp, f1 = std::min<int64_t>(n_frames, (s0 + n + spp - 1) / spp);
+            for (int64_t fa = f0; fa < f1; fa += 65535)
+                HIP_TRY(prt::launch_reduce((const float*)cx->buf.p, d_acc, (int)n_slots, s0, n, spp, fa,
+                                           std::min<int64_t>(65535, f1 - fa), accumulate, stream));
         }
     }
     return PRT_OK;

@@ -99,7 +99,10 @@ hipError_t launch_rays_prep(const TraceParams& P, const float* in8, int64_t n, i
                             float4* ray_o, hipStream_t stream);
 size_t lds_scene_bytes(const TraceParams& P);  // LDS-resident scene + shading data
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
-hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream);
+// per-frame sample-order sums of one chunk of launch samples [j0, j0 + n): frames f0 .. f0 + n_frames - 1
+// (frame f = launch samples [f spp, (f + 1) spp)) into acc + f n_slots 3, in one launch
+hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int64_t j0, int64_t n, int64_t spp, int64_t f0,
+                         int64_t n_frames, bool accumulate, hipStream_t stream);
 // packed tile slots (tile origins tile_xy) -> [x][y] window of the frame (prt_render, prt_render_multi)
 hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_slots, int log_tw, int log_tpx, int x0,
                           int y0, int w, int h, float* out, hipStream_t stream);

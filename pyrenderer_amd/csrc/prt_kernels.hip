@@ -197,11 +197,21 @@ __global__ __launch_bounds__(kBlock) void scatter_kernel(const float* __restrict
 }
 
 // Sequential per-pixel sum over this chunk's samples, in sample order, onto
-// the running sums (bit-identical to acc = acc + L[s] for s = 0..spp-1).
-__global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict__ buf, float* __restrict__ acc,
-                                                        int n_slots, int n_spp, int first) {
+// the running sums (bit-identical to acc = acc + L[s] for s = 0..spp-1).  One launch covers every
+// frame the chunk touches (blockIdx.y): frame f = f0 + y owns the chunk's launch samples
+// [max(j0, f spp), min(j0 + n, (f + 1) spp)), summed into acc + f n_slots 3; a frame's first
+// samples start its sums (unless accumulating), later chunks continue them.
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict__ buf, float* __restrict__ acc0,
+                                                        int n_slots, int64_t j0, int64_t n, int64_t spp, int64_t f0,
+                                                        int accumulate) {
     int slot = blockIdx.x * kBlock + threadIdx.x;
     if (slot >= n_slots) return;
+    const int64_t f = f0 + blockIdx.y;
+    const int64_t a = max(j0, f * spp), e = min(j0 + n, (f + 1) * spp);
+    const int n_spp = (int)(e - a);
+    const int first = (a == f * spp) && !accumulate;
+    buf += (size_t)(a - j0) * n_slots * 3;
+    float* __restrict__ acc = acc0 + (size_t)f * n_slots * 3;
     float r = 0.0f, g = 0.0f, b = 0.0f;
     if (!first) { r = acc[3 * (size_t)slot]; g = acc[3 * (size_t)slot + 1]; b = acc[3 * (size_t)slot + 2]; }
     for (int s = 0; s < n_spp; ++s) {
@@ -294,9 +304,11 @@ hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream)
     return hipGetLastError();
 }
 
-hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int n_spp, bool first, hipStream_t stream) {
-    int grid = (n_slots + kBlock - 1) / kBlock;
-    reduce_kernel<<<grid, kBlock, 0, stream>>>(buf, acc, n_slots, n_spp, first ? 1 : 0);
+hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int64_t j0, int64_t n, int64_t spp, int64_t f0,
+                         int64_t n_frames, bool accumulate, hipStream_t stream) {
+    if (n_frames <= 0 || n_frames > 65535) return hipErrorInvalidValue;
+    dim3 grid((unsigned)((n_slots + kBlock - 1) / kBlock), (unsigned)n_frames);
+    reduce_kernel<<<grid, kBlock, 0, stream>>>(buf, acc, n_slots, j0, n, spp, f0, accumulate ? 1 : 0);
     return hipGetLastError();
 }
 
