@@ -37,34 +37,37 @@ class TileShard:
         self.buf = self.bufs[0]
         self.host_staging = bool(host_staging) and self.buf.is_cuda
         self.wire = torch.empty_like(self.bufs, device="cpu") if self.host_staging else self.bufs
-        self.gather_lists = None
         self.gathered = None
         if world > 1 and rank == 0:
-            # per frame one contiguous receive buffer, rank-major with a stride of max_tiles tiles:
-            # the device scatter then reads every rank's tiles in one kernel (padding slots: id -1)
-            self.gathered = torch.empty((self.frames, world, self.bufs.shape[1]), dtype=torch.float32,
+            # one contiguous receive buffer [rank][frame][slots]: a group's frames arrive in ONE
+            # gather, and frame f's tiles of every rank sit at the same offsets from
+            # gathered[0, f], rank r's block a stride of frames * max_tiles tiles further on
+            self.gathered = torch.empty((world, self.frames, self.bufs.shape[1]), dtype=torch.float32,
                                         device=self.wire.device)
-            self.gather_lists = [list(self.gathered[f].unbind(0)) for f in range(self.frames)]
-        self.gather_list = self.gather_lists[0] if self.gather_lists else None
         self.per_rank = [interleaved_tiles(W, H, tile, r, world, scheme) for r in range(world)]
-        ids = np.full((world, self.max_tiles), -1, np.int32)
+        # scatter tile list seen from frame f's base: rank r's tile t at position (r * frames) *
+        # max_tiles + t, every other position (other frames' tiles, padding) id -1 (dropped)
+        ids = np.full((world, self.frames, self.max_tiles), -1, np.int32)
         for r, t in enumerate(self.per_rank):
-            ids[r, :len(t)] = t
-        self.scatter_ids = ids.reshape(-1)
+            ids[r, 0, :len(t)] = t
+        self.scatter_ids = ids.reshape(-1)[:((world - 1) * self.frames + 1) * self.max_tiles]
         self.frame_out = None    # rank 0's device frames (frames, W, H, 3), allocated by scatter()
-        self.packed_dev = None   # gloo: a gathered host buffer's device copy
+        self.packed_dev = None   # gloo: the gathered host buffer's device copy
+
+    def gather_list(self, n_frames=1):
+        """Rank 0's receive views for a gather of frames 0 .. n_frames-1 (None elsewhere)."""
+        return list(self.gathered[:, :n_frames].unbind(0)) if self.gathered is not None else None
 
     def gather(self, group=None, n_frames=1):
-        """Collective: rank 0 receives every rank's tile sums of frames 0 .. n_frames-1, one
-        gather per frame (no-op for world 1).  Runs on torch's current stream: callers that
-        rendered on another stream enter it first, and a later scatter() on the same stream is
-        ordered after the receive (ProcessGroupNCCL makes the current stream wait for its
-        collective stream when the work is enqueued)."""
+        """Collective: rank 0 receives every rank's tile sums of frames 0 .. n_frames-1 in ONE
+        gather (no-op for world 1).  Runs on torch's current stream: callers that rendered on
+        another stream enter it first, and a later scatter() on the same stream is ordered after
+        the receive (ProcessGroupNCCL makes the current stream wait for its collective stream
+        when the work is enqueued)."""
         if self.world > 1:
             if self.host_staging:
                 self.wire[:n_frames].copy_(self.bufs[:n_frames])   # synchronous device-to-host copy
-            for f in range(n_frames):
-                dist.gather(self.wire[f], self.gather_lists[f] if self.gather_lists else None, dst=0, group=group)
+            dist.gather(self.wire[:n_frames], self.gather_list(n_frames), dst=0, group=group)
 
     @property
     def frame(self):
@@ -72,10 +75,10 @@ class TileShard:
 
     def scatter(self, device_scene, stream=None, f=0):
         """Rank 0 after gather(): every rank's tiles of frame f -> the (W, H, 3) device frame
-        `frame_out[f]` by libprt's scatter kernel (prt_scatter_tiles, one launch over the
-        rank-major gathered buffer), enqueued on `stream` (default: torch's current stream).
-        gloo's host buffer is first uploaded on that stream.  This is the root-side step of
-        SURVEY.md §8(e) that bench.py times inside every N > 1 step."""
+        `frame_out[f]` by libprt's scatter kernel (prt_scatter_tiles, one launch over the gathered
+        buffer from frame f's base), enqueued on `stream` (default: torch's current stream).
+        gloo's host buffer is first uploaded on that stream (once per group, with frame 0).  This is
+        the root-side step of SURVEY.md §8(e) that bench.py times inside every N > 1 step."""
         dev = torch.device("cuda", device_scene.device)
         s = stream or torch.cuda.current_stream(dev)
         with torch.cuda.stream(s):
@@ -84,16 +87,18 @@ class TileShard:
             if self.frame_out is None:
                 self.frame_out = torch.zeros((self.frames, self.W, self.H, 3), dtype=torch.float32, device=dev)
             if self.world == 1:
-                packed = self.bufs[f]
-            elif self.gathered.is_cuda:
-                packed = self.gathered[f]
+                base = self.bufs[f]
             else:
-                if self.packed_dev is None:
-                    self.packed_dev = torch.empty(self.gathered[0].numel(), dtype=torch.float32, device=dev)
-                self.packed_dev.copy_(self.gathered[f].reshape(-1))
-                packed = self.packed_dev
+                packed = self.gathered
+                if not packed.is_cuda:
+                    if self.packed_dev is None:
+                        self.packed_dev = torch.empty_like(self.gathered, device=dev)
+                    if f == 0:
+                        self.packed_dev.copy_(self.gathered)
+                    packed = self.packed_dev
+                base = packed[0, f]
         ids = self.scatter_ids if self.world > 1 else self.per_rank[0]
-        device_scene.scatter_tiles(packed.data_ptr(), ids, self.tile, self.tile, self.W, self.H,
+        device_scene.scatter_tiles(base.data_ptr(), ids, self.tile, self.tile, self.W, self.H,
                                    self.frame_out[f].data_ptr(), s.cuda_stream)
         return self.frame_out[f]
 
@@ -104,7 +109,7 @@ class TileShard:
         the frame — the gathered tiles never pass through a host loop.  Without it (CPU-tensor
         shards: the gloo tests with the CPU oracle as renderer) the tiles are unpacked in numpy."""
         if device_scene is None:
-            bufs = self.gather_lists[f] if self.world > 1 else [self.bufs[f]]
+            bufs = [self.gathered[r, f] for r in range(self.world)] if self.world > 1 else [self.bufs[f]]
             frame = np.zeros((self.W, self.H, 3), np.float32)
             for b, ids in zip(bufs, self.per_rank):
                 n = len(ids) * self.slot_elems
@@ -112,6 +117,8 @@ class TileShard:
             return frame
         dev = torch.device("cuda", device_scene.device)
         s = stream or torch.cuda.current_stream(dev)
+        if self.world > 1 and not self.gathered.is_cuda and f != 0:
+            self.scatter(device_scene, s, 0)    # uploads the gloo host buffer for this group
         frame = self.scatter(device_scene, s, f)
         with torch.cuda.stream(s):
             out = frame.cpu().numpy()

@@ -17,5 +17,8 @@ else
   for c in 1 3 5; do bash tools/profile_bench.sh $c $O/prof_c$c; done
   bash tools/pmc_mem.sh 2 $O/pmc_mem_c2
   bash tools/pmc_mem.sh 4 $O/pmc_mem_c4
+  timeout -k 10 300 python tools/shard_sim.py --config 2 --tiles 16 --schemes latin --worlds 2,4,8 --proxy stream \
+    --streams 1 --frames 16 --steps 32 > $O/shard_f16.jsonl 2> $O/shard_f16.err
+  cat $O/shard_f16.jsonl
 fi
 echo ok

@@ -27,8 +27,8 @@ def main():
     ap.add_argument("--streams", type=int, default=1, help="frames in flight, as bench.py --streams")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--frames", type=int, default=1,
-                    help="frames per render call (prt_render_frames_device, bench.py --frames-per-launch); "
-                         "--steps is then a multiple of it")
+                    help="frames per render call (prt_render_frames_device, bench.py --frames-per-launch), "
+                         "gathered by one collective; --steps is then a multiple of it")
     ap.add_argument("--proxy", default="none", choices=("none", "stream", "stream-hp", "stream-nowait", "inline"),
                     help="after each frame, a copy of its tile buffer standing in for the RCCL gather: 'stream' on "
                          "one extra stream, ordered as torch's ProcessGroupNCCL orders a collective (the extra stream "
@@ -88,7 +88,7 @@ def main():
     def time_tiles(tile, ids):
         n = max(len(ids), 1) * tile * tile * 3
         bufs = [torch.empty(F * n, dtype=torch.float32, device=dev) for _ in streams]
-        dst = torch.empty(n, dtype=torch.float32, device=dev)
+        dst = torch.empty(F * n, dtype=torch.float32, device=dev)
         for b, st in zip(bufs, streams):
             render(ids, tile, b, st, 0)
         torch.cuda.synchronize(dev)
@@ -98,8 +98,7 @@ def main():
         for i in range(groups):
             k = i % len(streams)
             render(ids, tile, bufs[k], streams[k], N.PRT_FLAG_TIME)
-            for f in range(F):   # one gather per frame
-                gather_proxy(bufs[k][f * n:(f + 1) * n], streams[k], dst)
+            gather_proxy(bufs[k], streams[k], dst)   # one gather per group of F frames (bench.py)
         torch.cuda.synchronize(dev)
         wall = (time.perf_counter() - t0) * 1e3 / (groups * F)
         kms, launches = ds.kernel_timing()
