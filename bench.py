@@ -350,7 +350,7 @@ def main():
     rflags = (args.variant << 8) | (N.PRT_FLAG_NO_PRIMARY_KERNEL if args.no_primary_kernel else 0)
 
     def steps(nf, flags=0):
-        """nf (<= F) steps: nf frames rendered by one render call, then each frame's gather to rank 0
+        """nf (<= F) steps: nf frames rendered by one render call, then one gather of them to rank 0
         and (root) its device scatter into the (W, H, 3) frame."""
         k = n_step[0] % n_streams
         n_step[0] += 1
