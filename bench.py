@@ -104,8 +104,6 @@ def parse():
                          "on one GPU)")
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--no-primary-kernel", action="store_true",
-                    help="A/B: camera rays generated inside the trace kernel (PRT_FLAG_NO_PRIMARY_KERNEL)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
     ap.add_argument("--numpy-seconds", type=float, default=8.0,
                     help="target wall time of the NumPy-path CPU sample (main.py counterpart); 0 = skip")
@@ -347,7 +345,7 @@ def main():
     shards = [TileShard(W, H, T, rank, world, dev, args.scheme, host_staging=gloo, frames=F) for _ in range(n_streams)]
     my_tiles = shards[0].tiles
     n_step = [0]
-    rflags = (args.variant << 8) | (N.PRT_FLAG_NO_PRIMARY_KERNEL if args.no_primary_kernel else 0)
+    rflags = args.variant << 8
 
     def steps(nf, flags=0):
         """nf (<= F) steps: nf frames rendered by one render call, then one gather of them to rank 0

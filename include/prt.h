@@ -47,7 +47,10 @@ extern "C" {
 /* render flags */
 #define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
 #define PRT_FLAG_TIME 0x2u   /* time the trace kernel with HIP events on its stream */
-#define PRT_FLAG_NO_PRIMARY_KERNEL 0x4u /* generate camera rays inside the trace kernel (A/B; same image) */
+/* round 4: rejected with PRT_ERR_UNSUP — camera rays (and, for cameras other than the affine pinhole,
+ * their origins) always come from the camera kernel; the trace kernels carry no camera code, whose
+ * uniform operands spilled SGPRs in their loops (C2 4.01 -> 3.91 ms per launch without it) */
+#define PRT_FLAG_NO_PRIMARY_KERNEL 0x4u
 /* estimator variant: direct lighting by the reference's unused MIS function
  * PathTracer.sample_direct_lighting2 (core/tracing.py:57-90, helpers :12-39) in place of
  * sample_direct_lighting — two closest-hit visibility queries per diffuse vertex (light

@@ -91,7 +91,7 @@ struct DevBuf {
 // work counter + watchdog flag, the spill area and the host-output sums.
 struct RenderCtx {
     hipStream_t stream = nullptr;
-    DevBuf tiles, buf, rays, work, acc, spill;
+    DevBuf tiles, buf, rays, rays_o, work, acc, spill;
     std::vector<uint32_t> tile_host;   // tile origins of the last upload (== device copy in `tiles`)
     uint64_t last_use = 0;
 };
@@ -168,7 +168,7 @@ void destroy_scene(Scene* s) {
         b->release();
     if (!s->ctx.empty()) (void)hipDeviceSynchronize();
     for (auto& c : s->ctx)
-        for (DevBuf* b : {&c->tiles, &c->buf, &c->rays, &c->work, &c->acc, &c->spill})
+        for (DevBuf* b : {&c->tiles, &c->buf, &c->rays, &c->rays_o, &c->work, &c->acc, &c->spill})
             b->release();
     for (hipEvent_t e : s->ev) (void)hipEventDestroy(e);
     if (s->scatter_ev) (void)hipEventDestroy(s->scatter_ev);
@@ -387,6 +387,9 @@ int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, int64_t n_items, prt::T
 int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
                    int n_tiles, int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc,
                    int first_sample = 0, bool accumulate = false, int n_frames = 1, int frame_stride = 0) {
+    if (flags & PRT_FLAG_NO_PRIMARY_KERNEL)
+        return fail(PRT_ERR_UNSUP, "PRT_FLAG_NO_PRIMARY_KERNEL: camera rays always come from the camera kernel "
+                                   "(the trace kernels no longer carry camera code)");
     const int64_t n_slots = (int64_t)n_tiles * tw * th;
     if (n_slots == 0) return PRT_OK;
     hipStream_t stream = cx->stream;
@@ -411,18 +414,18 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     }
     // the launches' sample space: j = f * spp + (sample of frame f), T of them
     const int64_t T = (int64_t)spp * n_frames;
-    // per-sample buffers: radiance (12 B) + primary ray (16 B, pinhole cameras)
+    // per-sample buffers: radiance (12 B) + primary ray (16 B) + its origin (16 B, cameras other than
+    // the affine pinhole, whose origin is uniform)
     const bool cam_fast = camera_is_fast(cam);
-    const bool primary = cam_fast && !(flags & PRT_FLAG_NO_PRIMARY_KERNEL);
     int64_t per_sample = n_slots * 3 * (int64_t)sizeof(float);
-    int64_t per_sample_all = per_sample + (primary ? n_slots * 16 : 0);
+    int64_t per_sample_all = per_sample + n_slots * (cam_fast ? 16 : 32);
     // per-launch budget: the scene's (<= 16 GiB), and when this context's buffers must grow, at
     // most half of the device memory free now plus what they already hold — every render stream
     // (up to kMaxCtx) owns such a buffer set, so a budget fixed at scene creation could ask
     // several streams' worth of the memory that was free then
     size_t budget = s->chunk_bytes;
     {
-        const size_t held = cx->buf.bytes + cx->rays.bytes;
+        const size_t held = cx->buf.bytes + cx->rays.bytes + cx->rays_o.bytes;
         size_t free_b = 0, total_b = 0;
         if ((size_t)(std::min<int64_t>(T, (int64_t)(budget / (size_t)per_sample_all)) * per_sample_all) > held &&
             hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
@@ -437,19 +440,19 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         chunk = (T + nc - 1) / nc;
     }
     HIP_TRY(cx->buf.ensure((size_t)(chunk * per_sample)));
-    if (primary) HIP_TRY(cx->rays.ensure((size_t)(chunk * n_slots * 16)));
+    HIP_TRY(cx->rays.ensure((size_t)(chunk * n_slots * 16)));
+    if (!cam_fast) HIP_TRY(cx->rays_o.ensure((size_t)(chunk * n_slots * 16)));
     const bool stats = (flags & PRT_FLAG_STATS) != 0;
     const bool timed = (flags & PRT_FLAG_TIME) != 0;
     if (stats) HIP_TRY(hipMemsetAsync(s->stats.p, 0, kStatWords * sizeof(unsigned long long), stream));
-    // the watchdog flag is cleared once per render: by the first chunk's camera kernel, else here
-    if (!primary) HIP_TRY(hipMemsetAsync((char*)cx->work.p + kFaultOffset, 0, sizeof(int), stream));
 
     prt::TraceParams P;
     scene_params(s, P);
     std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
     {
         P.cam_fast = cam_fast ? 1 : 0;
-        P.rays = primary ? (const float4*)cx->rays.p : nullptr;
+        P.rays = (const float4*)cx->rays.p;
+        P.ray_o = cam_fast ? nullptr : (const float4*)cx->rays_o.p;
         const float rd2 = -cam[18];
         for (int i = 0; i < 3; ++i) {
             const float* c = cam + 4 * i;
@@ -490,15 +493,11 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
         P.n_items = (uint64_t)(n * n_slots);
         int64_t blocks_needed = ((int64_t)P.n_items + 255) / 256;
         int grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)occ * s->cus, blocks_needed));
-        if (primary) {
-            // the camera kernel also zeroes the work counter (and, for the first chunk, the
-            // watchdog flag) ahead of the trace launch: two fewer stream operations per frame
-            P.cam_clears = 1 | (s0 == 0 ? 2 : 0);
-            HIP_TRY(prt::launch_camera(P, (float4*)cx->rays.p, stream));
-            P.cam_clears = 0;
-        } else {
-            HIP_TRY(hipMemsetAsync(cx->work.p, 0, 16, stream));
-        }
+        // the camera kernel also zeroes the work counter (and, for the first chunk, the watchdog
+        // flag) ahead of the trace launch: two fewer stream operations per frame
+        P.cam_clears = 1 | (s0 == 0 ? 2 : 0);
+        HIP_TRY(prt::launch_camera(P, (float4*)cx->rays.p, cam_fast ? nullptr : (float4*)cx->rays_o.p, stream));
+        P.cam_clears = 0;
         if (timed) HIP_TRY(hipEventRecord(s->ev[2 * k], stream));
         DevBuf wclk;
         if (!s->wave_clock_path.empty()) {

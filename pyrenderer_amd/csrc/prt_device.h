@@ -952,21 +952,19 @@ void trace_kernel(TraceParams P) {
                 asm volatile("" : "+s"(W), "+s"(H));
                 bool ok = x < W && y < H;
                 if (ok) {
-                    if (P.rays) {
-                        float4 r = P.rays[item];
-                        d = v3(r.x, r.y, r.z);
-                        st = __float_as_uint(r.w);
-                        if (P.ray_o) {
-                            // prt_trace_rays: the caller's origin per ray (PathTracer.trace)
-                            const float4 ro = P.ray_o[item];
-                            o = v3(ro.x, ro.y, ro.z);
-                        } else {
-                            float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
-                            asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
-                            o = v3(o0, o1, o2);
-                        }
+                    // primary rays from camera_kernel (or prt_trace_rays' caller rays): no camera code
+                    // in the persistent loop, whose uniform operands would spill SGPRs
+                    float4 r = P.rays[item];
+                    d = v3(r.x, r.y, r.z);
+                    st = __float_as_uint(r.w);
+                    if (P.ray_o) {
+                        // per-ray origins: prt_trace_rays' caller rays, thin-lens / projective cameras
+                        const float4 ro = P.ray_o[item];
+                        o = v3(ro.x, ro.y, ro.z);
                     } else {
-                        camera_ray(P, x, y, chunk_s, st, o, d);
+                        float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
+                        asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
+                        o = v3(o0, o1, o2);
                     }
                 }
                 if (!ok) {
@@ -1551,20 +1549,18 @@ void trace_kernel_pool(TraceParams P) {
                     asm volatile("" : "+s"(W), "+s"(H));
                     bool ok = x < W && y < H;
                     if (ok) {
-                        if (P.rays) {
-                            float4 r = P.rays[item];
-                            d = v3(r.x, r.y, r.z);
-                            st = __float_as_uint(r.w);
-                            if (P.ray_o) {
-                                const float4 ro = P.ray_o[item];
-                                o = v3(ro.x, ro.y, ro.z);
-                            } else {
-                                float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
-                                asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
-                                o = v3(o0, o1, o2);
-                            }
+                        // primary rays from camera_kernel (or caller rays): no camera code in the loop —
+                        // its uniform operands spilled 36 more SGPRs (C2 4.01 -> 3.91 ms without it)
+                        float4 r = P.rays[item];
+                        d = v3(r.x, r.y, r.z);
+                        st = __float_as_uint(r.w);
+                        if (P.ray_o) {
+                            const float4 ro = P.ray_o[item];
+                            o = v3(ro.x, ro.y, ro.z);
                         } else {
-                            camera_ray(P, x, y, chunk_s, st, o, d);
+                            float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
+                            asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
+                            o = v3(o0, o1, o2);
                         }
                     }
                     if (!ok) {

@@ -87,7 +87,9 @@ bool variant_quantized(int var);
 
 int stack_variant(int bvh_depth);
 size_t trace_smem_bytes(int stack, int var, const TraceParams& P);
-hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream);
+// camera rays of a launch: rays = (d, rng state); ray_o = per-ray origins (cameras other than the affine
+// pinhole; null otherwise)
+hipError_t launch_camera(const TraceParams& P, float4* rays, float4* ray_o, hipStream_t stream);
 hipError_t launch_hits(const TraceParams& P, bool quantized, bool any, int stack, const float4* rays, int64_t n,
                        int* hit_id, float* hit_t, hipStream_t stream);
 // World.hit_all's shading at the closest hits of launch_hits (prt_hit_all): n x 16 f32

@@ -33,9 +33,10 @@ namespace {
 
 // Primary rays of one launch, generated with every lane busy (the persistent
 // trace kernel would otherwise run this code with the few lanes it refills):
-// rays[item] = (d, rng state after the camera draws).  Pinhole cameras only
-// (TraceParams::cam_fast), whose origin is the uniform cam_o.
-__global__ __launch_bounds__(kBlock) void camera_kernel(TraceParams P, float4* __restrict__ rays) {
+// rays[item] = (d, rng state after the camera draws); for cameras other than the affine pinhole
+// (TraceParams::cam_fast: the uniform origin cam_o) also ray_o[item] = the ray's origin.
+__global__ __launch_bounds__(kBlock) void camera_kernel(TraceParams P, float4* __restrict__ rays,
+                                                        float4* __restrict__ ray_o) {
     uint64_t item = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (P.cam_clears & 1) { P.work[0] = 0u; P.work[1] = 0u; P.work[2] = 0u; P.work[3] = 0u; }
@@ -61,6 +62,10 @@ __global__ __launch_bounds__(kBlock) void camera_kernel(TraceParams P, float4* _
     typedef float f4v __attribute__((ext_vector_type(4)));
     f4v r4 = {d.x, d.y, d.z, __uint_as_float(st)};
     __builtin_nontemporal_store(r4, reinterpret_cast<f4v*>(rays + item));
+    if (ray_o) {
+        f4v o4 = {o.x, o.y, o.z, 0.0f};
+        __builtin_nontemporal_store(o4, reinterpret_cast<f4v*>(ray_o + item));
+    }
 }
 
 // World.hit_all for a batch of rays (intersection_taichi.py:238-291): closest (or any)
@@ -298,9 +303,9 @@ hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_sl
     return hipGetLastError();
 }
 
-hipError_t launch_camera(const TraceParams& P, float4* rays, hipStream_t stream) {
+hipError_t launch_camera(const TraceParams& P, float4* rays, float4* ray_o, hipStream_t stream) {
     int64_t grid = ((int64_t)P.n_items + kBlock - 1) / kBlock;
-    camera_kernel<<<(unsigned)grid, kBlock, 0, stream>>>(P, rays);
+    camera_kernel<<<(unsigned)grid, kBlock, 0, stream>>>(P, rays, ray_o);
     return hipGetLastError();
 }
 

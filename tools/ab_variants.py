@@ -17,10 +17,8 @@ sys.path.insert(0, ROOT)
 
 
 def vflags(v):
-    """'15' -> variant 15; '15np' -> variant 15 with camera rays generated inside the trace kernel."""
-    from pyrenderer_amd._native import PRT_FLAG_NO_PRIMARY_KERNEL
-    np_ = v.endswith("np")
-    return (int(v[:-2] if np_ else v) << 8) | (PRT_FLAG_NO_PRIMARY_KERNEL if np_ else 0)
+    """'7' -> variant 7's flag bits."""
+    return int(v) << 8
 
 
 def main():
@@ -30,7 +28,7 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", nargs="+", default=["1", "2", "3"],
-                    help="kernel variant numbers; suffix 'np' = camera rays inside the trace kernel")
+                    help="kernel variant numbers")
     ap.add_argument("--scene", default="cornell", help="cornell | cubes | soup:N (random triangle soup of N tris in the box)")
     a = ap.parse_args()
     from pyrenderer_amd._native import PRT_FLAG_TIME
