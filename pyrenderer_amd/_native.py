@@ -12,10 +12,11 @@ from .build import LIB
 
 ABI_VERSION = 2        # include/prt.h PRT_ABI_VERSION
 PRT_OK = 0
+PRT_ERR_UNSUP = -5      # feature not supported by this build
 PRT_ERR_INTERNAL = -6   # device-side check failed (traversal watchdog)
 PRT_FLAG_STATS = 0x1
 PRT_FLAG_TIME = 0x2
-PRT_FLAG_NO_PRIMARY_KERNEL = 0x4
+PRT_FLAG_NO_PRIMARY_KERNEL = 0x4   # rejected (PRT_ERR_UNSUP) since round 4: camera rays come from the camera kernel
 PRT_FLAG_MIS_NEE = 0x8
 # trace-kernel variant ids 1..VAR_LAST of the reference estimator (pyrenderer_amd/csrc/prt_kernels.h
 # kVar*); the MIS direct-lighting estimator's variants (PRT_FLAG_MIS_NEE) follow

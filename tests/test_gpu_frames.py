@@ -77,3 +77,17 @@ def test_frames_argument_checks(gpu_scene, cornell):
     for n, stride in ((0, 0), (2, -1)):
         with pytest.raises(PrtError):
             gpu_scene.render_frames_device(packed, 8, 8, 8, 8, [0], 1, 1, n, out.data_ptr(), frame_stride=stride)
+
+
+def test_in_kernel_camera_flag_is_rejected(gpu_scene, cornell):
+    """PRT_FLAG_NO_PRIMARY_KERNEL is gone from the trace kernels (round 4): an explicit error, not a
+    silently different path."""
+    import torch
+    from pyrenderer_amd._native import PrtError, PRT_FLAG_NO_PRIMARY_KERNEL, PRT_ERR_UNSUP
+    scene, cam, flat = cornell
+    packed = cam.convert_to_taichi_camera().packed()
+    out = torch.zeros(64 * 3, dtype=torch.float32, device="cuda:0")
+    with pytest.raises(PrtError) as e:
+        gpu_scene.render_frames_device(packed, 8, 8, 8, 8, [0], 1, 1, 1, out.data_ptr(),
+                                       flags=PRT_FLAG_NO_PRIMARY_KERNEL)
+    assert e.value.code == PRT_ERR_UNSUP

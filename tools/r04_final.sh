@@ -14,6 +14,8 @@ if [ "${2:-a}" = a ]; then
   for c in 2 4; do bash tools/profile_bench.sh $c $O/prof_c$c; done
   bash tools/bench_all.sh $O/bench_all
 else
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_frames.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_frames.log 2>&1
+  tail -2 $O/pytest_frames.log
   for c in 1 3 5; do bash tools/profile_bench.sh $c $O/prof_c$c; done
   bash tools/pmc_mem.sh 2 $O/pmc_mem_c2
   bash tools/pmc_mem.sh 4 $O/pmc_mem_c4
