@@ -516,7 +516,7 @@ def main():
                        "baseline_config": args.config, "triangles": int(flat.n_tri), "spheres": int(flat.sph.shape[0]),
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
                        "backend": (args.backend if world > 1 else None),
-                       "tile_scheme": args.scheme, "frames_in_flight": n_streams, "frames_per_launch": F,
+                       "tile_scheme": args.scheme, "frames_in_flight": n_streams, "frames_per_launch": -(-args.steps // -(-args.steps // F)),
                        "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
             "roofline": roofline,
             "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),
