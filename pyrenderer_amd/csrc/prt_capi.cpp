@@ -124,6 +124,7 @@ struct Scene {
     int spill_lds = 16;              // LDS part of the spill variants' stack (env PRT_SPILL_LDS: 4, 16 or 32)
     std::string wave_clock_path;     // env PRT_WAVE_CLOCK: append each trace launch's per-wave clocks here
     int64_t n_sph = 0;
+    bool plain = false;              // no spheres, no metal / dielectric material (TraceParams::plain)
     DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
     hipStream_t stream = nullptr;
     std::vector<std::unique_ptr<RenderCtx>> ctx;  // per render stream (<= kMaxCtx)
@@ -318,6 +319,7 @@ void scene_params(Scene* s, prt::TraceParams& P) {
     P.n_sph = (int)s->n_sph;
     P.sph = (const float4*)s->sph.p;
     P.sph_mat = (const int*)s->sph_mat.p;
+    P.plain = s->plain ? 1 : 0;
     P.frame_spp = 0xFFFFFFFFu;   // one frame: global sample = s0 + j0 + the chunk's sample
 }
 
@@ -745,6 +747,9 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         if ((rc = upload(s->light_v, lv.data(), sizeof(float) * lv.size(), &s->device_bytes))) break;
         if ((rc = upload(s->light_off, light_off, sizeof(int32_t) * (size_t)(n_light + 1), &s->device_bytes))) break;
         s->n_sph = n_sph;
+        s->plain = n_sph == 0;
+        for (int32_t i = 0; i < n_mat; ++i)
+            if (mat[8 * i + 5] == 2.0f || mat[8 * i + 5] == 3.0f) s->plain = false;   // metal / dielectric
         if ((rc = upload(s->sph, sph, sizeof(float) * 4 * (size_t)n_sph, &s->device_bytes))) break;
         if ((rc = upload(s->sph_mat, sph_mat, sizeof(int32_t) * (size_t)n_sph, &s->device_bytes))) break;
         if ((e = s->work.ensure(64)) != hipSuccess || (e = s->stats.ensure(8 * kStatWords)) != hipSuccess) {

@@ -1459,7 +1459,10 @@ constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 
 // done by then); S waves run beside the other waves' next traversals, and waves without a chunk go
 // straight on to their refill (C2 4.049 vs 4.080 ms, C3 at 1024^2 x 32 spp 9.455 vs 9.570 ms per
 // launch against the two-barrier kernel, profiles/r04/pool1b/).
-template <bool STATS, int WPE>
+// PLAIN: the lean build for scenes without spheres and metal / dielectric materials (P.plain; C1, C2,
+// C5): without that code the kernel's loop keeps 17 fewer uniform values in spilled SGPRs and is a
+// third shorter
+template <bool STATS, int WPE, bool PLAIN>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel_pool(TraceParams P) {
     extern __shared__ float4 smem[];
@@ -1598,7 +1601,7 @@ void trace_kernel_pool(TraceParams P) {
                     g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
                 if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
-                if (P.n_sph > 0) {
+                if (!PLAIN && P.n_sph > 0) {
                     float best = hit ? ht : kTMax;
                     for (int k = 0; k < P.n_sph; ++k) {
                         float root;
@@ -1650,7 +1653,7 @@ void trace_kernel_pool(TraceParams P) {
                     V3 p = o + d * ht;
                     V3 ng;
                     int mid;
-                    if (hid < P.n_tri) {
+                    if (PLAIN || hid < P.n_tri) {
                         float4 nm = s_nm[hid];
                         ng = xyz(nm);
                         mid = __float_as_int(nm.w);
@@ -1663,7 +1666,7 @@ void trace_kernel_pool(TraceParams P) {
                     const float* m = s_mats + 8 * mid;
                     const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;
                     const V3 n = flip ? neg(ng) : ng;
-                    if (m[5] == 2.0f || m[5] == 3.0f) {
+                    if (!PLAIN && (m[5] == 2.0f || m[5] == 3.0f)) {
                         bool front = dot(d, ng) < 0.0f;
                         V3 ns = front ? ng : neg(ng);
                         V3 unit = normalize(d);
@@ -1701,8 +1704,8 @@ void trace_kernel_pool(TraceParams P) {
                         float u0 = rng_next(st);
                         float u1 = rng_next(st);
                         V3 l = cosine_hemisphere<true>(u0, u1);
-                        const float4* fr = s_fr + ((size_t)(hid < P.n_tri ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
-                        if (hid < P.n_tri) {
+                        const float4* fr = s_fr + ((size_t)((PLAIN || hid < P.n_tri) ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
+                        if (PLAIN || hid < P.n_tri) {
                             float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
                             wi = normalize<true>(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
                         } else {
@@ -1826,7 +1829,7 @@ void trace_kernel_pool(TraceParams P) {
                     g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
                 if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
-                if (P.n_sph > 0 && !hit) {
+                if (!PLAIN && P.n_sph > 0 && !hit) {
                     for (int k = 0; k < P.n_sph; ++k) {
                         float root;
                         if (sphere_hit(P.sph[k], so, sd, kTMin, stm, root)) { hit = true; break; }

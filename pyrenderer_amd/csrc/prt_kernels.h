@@ -59,6 +59,7 @@ struct TraceParams {
     // two memset launches per frame
     int cam_clears;
     int lds_stack;            // pool kernel: 16-bit LDS traversal stack entries per lane (>= the BVH4's need)
+    int plain;                // 1: no spheres and no metal / dielectric material (the pool kernel's lean build)
 };
 
 // trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the
@@ -110,6 +111,7 @@ hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_sl
                           int y0, int w, int h, float* out, hipStream_t stream);
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 // the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
+// the pooled kernel's lean instantiation (no sphere or specular code) runs when P.plain is set
 hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream);
 int trace_occ_pool(bool stats, int wpe, size_t smem);
 

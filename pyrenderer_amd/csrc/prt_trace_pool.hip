@@ -1,7 +1,7 @@
 // prt_trace_pool.hip — the block-pooled shadow-query trace kernel (prt_device.h trace_kernel_pool)
 // in its own compilation unit: pyrenderer_amd/build.py compiles it with LLVM's AMDGPU
 // register-pressure trackers (-mllvm --amdgpu-use-amdgpu-trackers), under which the kernel fits
-// the 72 VGPRs of 7 waves per SIMD with 4 spilled registers instead of 39 (the other trace
+// the 72 VGPRs of 7 waves per SIMD with 3 spilled registers instead of 39 (the other trace
 // kernels keep the default scheduler: the global-scene kernel is slower with the trackers,
 // DESIGN.md §2).
 #pragma clang fp contract(off)
@@ -10,27 +10,30 @@
 
 namespace prt {
 
-hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream) {
-    if (stats) {
-        if (wpe == 7) trace_kernel_pool<true, 7><<<grid, kBlock, smem, stream>>>(P);
-        else if (wpe == 6) trace_kernel_pool<true, 6><<<grid, kBlock, smem, stream>>>(P);
-        else return hipErrorInvalidValue;
-    } else {
-        if (wpe == 7) trace_kernel_pool<false, 7><<<grid, kBlock, smem, stream>>>(P);
-        else if (wpe == 6) trace_kernel_pool<false, 6><<<grid, kBlock, smem, stream>>>(P);
-        else return hipErrorInvalidValue;
-    }
+namespace {
+template <bool STATS, int WPE>
+hipError_t launch_pool(const TraceParams& P, int grid, size_t smem, hipStream_t stream) {
+    if (P.plain) trace_kernel_pool<STATS, WPE, true><<<grid, kBlock, smem, stream>>>(P);
+    else trace_kernel_pool<STATS, WPE, false><<<grid, kBlock, smem, stream>>>(P);
     return hipGetLastError();
 }
+}  // namespace
 
+hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream) {
+    if (wpe != 7 && wpe != 6) return hipErrorInvalidValue;
+    if (stats) return wpe == 7 ? launch_pool<true, 7>(P, grid, smem, stream) : launch_pool<true, 6>(P, grid, smem, stream);
+    return wpe == 7 ? launch_pool<false, 7>(P, grid, smem, stream) : launch_pool<false, 6>(P, grid, smem, stream);
+}
+
+// both builds fit the same blocks per CU (the waves-per-EU target and the LDS size set it)
 int trace_occ_pool(bool stats, int wpe, size_t smem) {
     int n = 0;
     if (stats) {
-        if (wpe == 7) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<true, 7>, kBlock, smem);
-        else if (wpe == 6) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<true, 6>, kBlock, smem);
+        if (wpe == 7) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<true, 7, false>, kBlock, smem);
+        else if (wpe == 6) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<true, 6, false>, kBlock, smem);
     } else {
-        if (wpe == 7) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<false, 7>, kBlock, smem);
-        else if (wpe == 6) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<false, 6>, kBlock, smem);
+        if (wpe == 7) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<false, 7, false>, kBlock, smem);
+        else if (wpe == 6) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, trace_kernel_pool<false, 6, false>, kBlock, smem);
     }
     return n;
 }

@@ -15,10 +15,10 @@ pytestmark = pytest.mark.gpu
 TOL_RMSE = 1e-3
 
 
-def _gpu_frame(ds, cam, W, H, spp, depth, seed=0, tile=64):
+def _gpu_frame(ds, cam, W, H, spp, depth, seed=0, tile=64, flags=0):
     from pyrenderer_amd.device_scene import interleaved_tiles, unpack_tiles
     ids = interleaved_tiles(W, H, tile)
-    sums, _ = ds.render_tiles(cam, W, H, tile, tile, ids, spp, depth, seed)
+    sums, _ = ds.render_tiles(cam, W, H, tile, tile, ids, spp, depth, seed, flags=flags)
     return unpack_tiles(sums, W, H, tile, tile, ids)
 
 
@@ -225,16 +225,19 @@ def _specular_scene(rough=0.0):
     return scene, cam, flatten_scene(scene)
 
 
-@pytest.mark.parametrize("rough", [0.0, 0.35])
-def test_specular_scene_matches_oracle(rough):
-    """Config 3's materials (metal, dielectric, sphere) through the C-ABI vs the oracle."""
+@pytest.mark.parametrize("rough,kernel", [(0.0, "default"), (0.35, "default"), (0.35, "pool")])
+def test_specular_scene_matches_oracle(rough, kernel):
+    """Config 3's materials (metal, dielectric, sphere) through the C-ABI vs the oracle; "pool"
+    forces the pooled kernel (its full build: a small frame otherwise takes the phase-aligned one)."""
+    from pyrenderer_amd import _native as N
     from pyrenderer_amd.device_scene import DeviceScene
     scene, cam, flat = _specular_scene(rough)
     assert flat.sph.shape[0] == 1 and (flat.mat[:, 5] == 2).any() and (flat.mat[:, 5] == 3).any()
     ds = DeviceScene(flat, 0)
     osc = O.OracleScene.from_flat(flat)
     c = cam.convert_to_taichi_camera().packed()
-    g = _gpu_frame(ds, c, 64, 64, 4, 8, seed=4)
+    flags = (N.VAR_LDS_POOL << 8) if kernel == "pool" else 0
+    g = _gpu_frame(ds, c, 64, 64, 4, 8, seed=4, flags=flags)
     o = osc.render(c, 64, 64, 4, 8, seed=4)
     assert np.isfinite(g).all() and g.sum() > 0
     rmse, same = _compare(g, o, 4)
