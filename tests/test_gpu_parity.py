@@ -211,7 +211,7 @@ def test_full_size_config2_matches_oracle(gpu_scene, oracle_scene, cornell):
     assert not diff.any(), (int(diff.sum()), np.argwhere(diff)[:5])
 
 
-def _specular_scene(rough=0.0):
+def _specular_scene(rough=0.0, spheres=True):
     import json
     import os
     from conftest import ROOT
@@ -221,6 +221,8 @@ def _specular_scene(rough=0.0):
     for b in d["bsdfs"]:
         if b["type"] == "metal":
             b["roughness"] = rough
+    if not spheres:
+        d["primitives"] = [p for p in d["primitives"] if p["type"] != "sphere"]
     scene, cam = process_primitives(d)
     return scene, cam, flatten_scene(scene)
 
@@ -240,6 +242,23 @@ def test_specular_scene_matches_oracle(rough, kernel):
     g = _gpu_frame(ds, c, 64, 64, 4, 8, seed=4, flags=flags)
     o = osc.render(c, 64, 64, 4, 8, seed=4)
     assert np.isfinite(g).all() and g.sum() > 0
+    rmse, same = _compare(g, o, 4)
+    assert rmse < TOL_RMSE, rmse
+    assert same >= 0.999, same
+
+
+def test_specular_boxes_without_spheres_take_the_full_pooled_build():
+    """Metal / dielectric boxes but no sphere: the pooled kernel's lean build (TraceParams::plain)
+    must not be chosen — it has no specular code — so the image still matches the oracle."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    scene, cam, flat = _specular_scene(0.35, spheres=False)
+    assert flat.sph.shape[0] == 0 and (flat.mat[:, 5] == 2).any() and (flat.mat[:, 5] == 3).any()
+    ds = DeviceScene(flat, 0)
+    osc = O.OracleScene.from_flat(flat)
+    c = cam.convert_to_taichi_camera().packed()
+    g = _gpu_frame(ds, c, 64, 64, 4, 8, seed=5, flags=N.VAR_LDS_POOL << 8)
+    o = osc.render(c, 64, 64, 4, 8, seed=5)
     rmse, same = _compare(g, o, 4)
     assert rmse < TOL_RMSE, rmse
     assert same >= 0.999, same
