@@ -359,14 +359,17 @@ def main():
         else:
             # consecutive progressive frames (main_taichi.py:108-118): frame f of the group renders
             # samples f * spp .. (f + 1) * spp - 1, so no two frames of a launch repeat work
+            # frame f -> shard.bufs[f]: the rows are padded to the largest shard (the gather's slot), so
+            # the render writes at that pitch (a ragged shard's frames would otherwise shift)
             ds.render_frames_device(cam, W, H, T, T, my_tiles, args.spp, args.depth, nf, shard.bufs.data_ptr(),
-                                    stream.cuda_stream, seed=args.seed, frame_stride=args.spp, flags=flags | rflags)
+                                    stream.cuda_stream, seed=args.seed, frame_stride=args.spp, flags=flags | rflags,
+                                    out_pitch=shard.pitch)
         with torch.cuda.stream(stream):
             shard.gather(n_frames=nf)    # RCCL gathers of per-tile radiance sums to rank 0 (ordered after the frames)
             if world > 1 and rank == 0:
-                # root: every rank's tiles into the (W, H, 3) device frames, inside the step
-                for f in range(nf):
-                    shard.scatter(ds, stream, f)
+                # root: every rank's tiles of the group's frames into the (W, H, 3) device frames
+                # (SURVEY.md §8(e)), one launch, inside the step
+                shard.scatter_frames(ds, stream, nf)
 
     def run(n):
         # equal groups of <= F frames (equal launches: the per-launch roofline averages like sizes)

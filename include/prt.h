@@ -28,13 +28,20 @@
 extern "C" {
 #endif
 
-/* ABI 2 (this build): prt_trace_rays, prt_hit_all added; trace-kernel variant ids renumbered
- * to 1..8 (PRT_FLAG_VARIANT; 7 / 8 are the pooled-shadow kernel; ids above 8 are rejected with
+/* ABI history.
+ * ABI 2: prt_trace_rays, prt_hit_all added; trace-kernel variant ids renumbered to 1..8
+ * (PRT_FLAG_VARIANT; 7 / 8 are the pooled-shadow kernel; ids above 8 are rejected with
  * PRT_ERR_ARG, and ABI 1's ids 1..8 named other kernels, so a caller built against ABI 1 must
- * check prt_abi_version());
- * prt_scene_info's info8[4] is the BVH4 LDS traversal stack depth (0: BVH4 too deep for
- * the LDS-stack variants); watchdog flags are cleared once reported (prt_check_faults). */
-#define PRT_ABI_VERSION 2
+ * check prt_abi_version()); prt_scene_info's info8[4] is the BVH4 LDS traversal stack depth (0:
+ * BVH4 too deep for the LDS-stack variants); watchdog flags are cleared once reported
+ * (prt_check_faults).
+ * ABI 3 (this build): prt_render_frames_device (round 4) takes an output pitch between frames
+ * (out_pitch, floats; 0 = packed), so a rank whose shard is shorter than its gather slot can render
+ * straight into a padded per-frame buffer; PRT_FLAG_NO_PRIMARY_KERNEL, accepted by ABI 2, is
+ * rejected with PRT_ERR_UNSUP; prt_scatter_frames added; variant ids 9 / 10 (the pooled kernel's
+ * fused schedule, 7 / 6 waves per SIMD: extension traversals also answer the pooled shadow rays)
+ * added, ids above 10 rejected with PRT_ERR_ARG. */
+#define PRT_ABI_VERSION 3
 
 #define PRT_OK 0
 #define PRT_ERR_ARG (-1)     /* invalid argument / shape */
@@ -47,7 +54,7 @@ extern "C" {
 /* render flags */
 #define PRT_FLAG_STATS 0x1u  /* count BVH nodes / triangle tests / queries (slower kernel variant) */
 #define PRT_FLAG_TIME 0x2u   /* time the trace kernel with HIP events on its stream */
-/* round 4: rejected with PRT_ERR_UNSUP — camera rays (and, for cameras other than the affine pinhole,
+/* ABI 3: rejected with PRT_ERR_UNSUP — camera rays (and, for cameras other than the affine pinhole,
  * their origins) always come from the camera kernel; the trace kernels carry no camera code, whose
  * uniform operands spilled SGPRs in their loops (C2 4.01 -> 3.91 ms per launch without it) */
 #define PRT_FLAG_NO_PRIMARY_KERNEL 0x4u
@@ -170,6 +177,15 @@ void prt_comm_release(void);
  * of the gathered buffers. */
 int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_ids, int n_tiles, int tw, int th,
                       int W, int H, float* d_frame, void* stream);
+/* ABI 3: the root's scatter of a whole multi-frame gather in ONE launch.  d_packed holds n_groups
+ * blocks (one per rank, rank r's at d_packed + r * group_pitch floats), each with n_frames frames of
+ * group_tiles tile slots (frame f at + f * src_frame_pitch floats); tile_ids = n_groups * group_tiles
+ * host ids (rank-major, -1 = padding).  Frame f goes to d_frames + f * W*H*3 floats ([x][y]).  The
+ * launch covers n_groups * group_tiles slots per frame: the per-rank padding of a ragged shard is
+ * one tile list, not (world - 1) * n_frames other frames' slots. */
+int prt_scatter_frames(void* scene, const float* d_packed, const int32_t* tile_ids, int n_groups, int group_tiles,
+                       int64_t group_pitch, int tw, int th, int W, int H, int n_frames, int64_t src_frame_pitch,
+                       float* d_frames, void* stream);
 /* Progressive rendering: main_taichi.py:108-127 runs render() once per GUI frame
  * (pixels[x,y] += L, samples[x,y] += 1) and displays the running mean.  This call
  * renders samples first_sample .. first_sample+spp-1 of every pixel (the same
@@ -194,14 +210,17 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
  * main_taichi.py:108-118, or repeated renders of one frame): frame f = samples
  * f * frame_stride + 0 .. spp - 1 of every pixel of the tile set (frame_stride = spp: consecutive
  * progressive frames; 0: n_frames renders of the same samples), its per-pixel sums written to
- * d_out_sums + f * n_tiles*tw*th*3 (device, slot order of prt_render_tiles).  Every frame is
+ * d_out_sums + f * out_pitch floats (device, slot order of prt_render_tiles; out_pitch 0 = packed
+ * frames, n_tiles*tw*th*3; otherwise >= that, e.g. the padded per-frame slot of a gather
+ * buffer — the floats between a frame's sums and the next frame are not written).  Every frame is
  * bit-identical to the prt_render_tiles_accumulate call of its samples from zero sums; the
  * launches carry all frames' (pixel, sample) items (as many frames per launch as the per-launch
  * buffer budget holds), so a persistent launch ramps up and drains once per launch instead of
  * once per frame.  Enqueued on `stream` like prt_render_tiles_device. */
 int prt_render_frames_device(void* scene, const float* cam, int W, int H, int tw, int th,
                              const int32_t* tile_ids, int n_tiles, int spp, int depth, uint64_t seed,
-                             int n_frames, int frame_stride, uint32_t flags, float* d_out_sums, void* stream);
+                             int n_frames, int frame_stride, uint32_t flags, float* d_out_sums, int64_t out_pitch,
+                             void* stream);
 /* trace-kernel time of every render call made with PRT_FLAG_TIME since the
  * previous prt_kernel_timing() (synchronises on their events, then resets):
  * total ms and number of trace launches.  Also reports PRT_ERR_INTERNAL if the

@@ -10,7 +10,7 @@ import numpy as np
 
 from .build import LIB
 
-ABI_VERSION = 2        # include/prt.h PRT_ABI_VERSION
+ABI_VERSION = 3        # include/prt.h PRT_ABI_VERSION
 PRT_OK = 0
 PRT_ERR_UNSUP = -5      # feature not supported by this build
 PRT_ERR_INTERNAL = -6   # device-side check failed (traversal watchdog)
@@ -27,9 +27,12 @@ VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
 VAR_LDS6 = 6          # VAR_LDS built for >= 6 waves/SIMD (LDS copies that fit 6 but not 7 blocks per CU)
 VAR_LDS_POOL = 7      # LDS-resident scene, block-pooled shadow queries (trace_kernel_pool)
 VAR_LDS_POOL6 = 8     # VAR_LDS_POOL built for >= 6 waves/SIMD
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6)
-VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6)
-VAR_LAST = 8
+VAR_LDS_FUSED = 9     # trace_kernel_pool's FUSED schedule: extension traversals also answer pooled shadow rays
+VAR_LDS_FUSED6 = 10   # VAR_LDS_FUSED built for >= 6 waves/SIMD
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_FUSED,
+                 VAR_LDS_FUSED6)
+VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_FUSED, VAR_LDS_FUSED6)
+VAR_LAST = 10
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 
@@ -70,8 +73,9 @@ EXPORTS = {
     "prt_render_multi": (_i, [_vp, _i, _vp, _i, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_comm_release": (None, []),
     "prt_scatter_tiles": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    "prt_scatter_frames": (_i, [_vp, _vp, _vp, _i, _i, _i64, _i, _i, _i, _i, _i, _i64, _vp, _vp]),
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
-    "prt_render_frames_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _i, _i, _u32, _vp, _vp]),
+    "prt_render_frames_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _i, _i, _u32, _vp, _i64, _vp]),
     "prt_render_tiles_accumulate": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_kernel_timing": (_i, [_vp, _vp, _vp]),
     "prt_check_faults": (_i, [_vp]),

@@ -68,8 +68,9 @@ void frame_rows(F3 n, float* out12) {
 }
 
 // stats words: nodes, tris, ext, shadow (public) + diagnostic wave clocks
-// (refill, traversal, shading), wave iterations, active lanes at traversal
-constexpr int kStatWords = 24 + 16 * 8;   // prt_diag_stats' 16 + prt_diag_words' extras (outlier log)
+// (refill, traversal, shading), wave iterations, active lanes at traversal; words 24..151 the outlier
+// log, 160..175 the pooled kernel's lane table (STATS builds)
+constexpr int kStatWords = 192;
 
 struct DevBuf {
     void* p = nullptr;
@@ -383,17 +384,20 @@ int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, int64_t n_items, prt::T
 // first_sample .. first_sample + spp - 1 of every pixel; `accumulate` adds them onto the
 // sums already in d_acc (progressive rendering) instead of overwriting them.
 // n_frames > 1 (prt_render_frames_device): frame f renders samples first_sample + f * frame_stride
-// + 0 .. spp - 1 into d_acc + f * n_slots * 3, and all frames' items run through the same
+// + 0 .. spp - 1 into d_acc + f * out_pitch floats (0: packed, n_slots * 3), and all frames' items run
+// through the same
 // persistent launches (a launch covers up to the memory budget's worth of frames), so the
 // launch drains once per launch instead of once per frame.
 int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
                    int n_tiles, int spp, int depth, uint64_t seed, uint32_t flags, float* d_acc,
-                   int first_sample = 0, bool accumulate = false, int n_frames = 1, int frame_stride = 0) {
+                   int first_sample = 0, bool accumulate = false, int n_frames = 1, int frame_stride = 0,
+                   int64_t out_pitch = 0) {
     if (flags & PRT_FLAG_NO_PRIMARY_KERNEL)
         return fail(PRT_ERR_UNSUP, "PRT_FLAG_NO_PRIMARY_KERNEL: camera rays always come from the camera kernel "
                                    "(the trace kernels no longer carry camera code)");
     const int64_t n_slots = (int64_t)n_tiles * tw * th;
     if (n_slots == 0) return PRT_OK;
+    if (out_pitch == 0) out_pitch = 3 * n_slots;
     hipStream_t stream = cx->stream;
     // per-tile pixel origins (x0 << 16 | y0); uploaded only when they differ from the
     // context's last upload (a bench or animation re-renders the same tile set every
@@ -411,7 +415,9 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
     }
     if (spp == 0 || depth == 0) {
         // every sample's radiance is 0: the sums are 0, or unchanged when accumulating
-        if (!accumulate) HIP_TRY(hipMemsetAsync(d_acc, 0, sizeof(float) * 3 * (size_t)n_slots * n_frames, stream));
+        if (!accumulate)
+            HIP_TRY(hipMemset2DAsync(d_acc, sizeof(float) * (size_t)out_pitch, 0, sizeof(float) * 3 * (size_t)n_slots,
+                                     (size_t)n_frames, stream));
         return PRT_OK;
     }
     // the launches' sample space: j = f * spp + (sample of frame f), T of them
@@ -526,7 +532,7 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
             const int64_t f0 = s0 / spp, f1 = std::min<int64_t>(n_frames, (s0 + n + spp - 1) / spp);
             for (int64_t fa = f0; fa < f1; fa += 65535)
                 HIP_TRY(prt::launch_reduce((const float*)cx->buf.p, d_acc, (int)n_slots, s0, n, spp, fa,
-                                           std::min<int64_t>(65535, f1 - fa), accumulate, stream));
+                                           std::min<int64_t>(65535, f1 - fa), out_pitch, accumulate, stream));
         }
     }
     return PRT_OK;
@@ -1027,7 +1033,7 @@ int prt_render_tiles_device(void* scene, const float* cam, int W, int H, int tw,
 
 int prt_render_frames_device(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
                              int n_tiles, int spp, int depth, uint64_t seed, int n_frames, int frame_stride,
-                             uint32_t flags, float* d_out_sums, void* stream) {
+                             uint32_t flags, float* d_out_sums, int64_t out_pitch, void* stream) {
     auto* s = (Scene*)scene;
     int rc = check_render_args(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth);
     if (rc) return rc;
@@ -1036,11 +1042,13 @@ int prt_render_frames_device(void* scene, const float* cam, int W, int H, int tw
     if ((int64_t)(n_frames - 1) * frame_stride + spp > INT32_MAX || (int64_t)n_frames * spp > INT32_MAX)
         return fail(PRT_ERR_ARG, "sample indices must stay below 2^31");
     if (!d_out_sums && n_tiles > 0) return fail(PRT_ERR_ARG, "d_out_sums is NULL");
+    if (out_pitch != 0 && out_pitch < 3 * (int64_t)n_tiles * tw * th)
+        return fail(PRT_ERR_ARG, "out_pitch must be 0 (packed frames) or >= n_tiles * tw * th * 3 floats");
     DeviceGuard g(s->device);
     RenderCtx* cx = ctx_for(s, stream ? (hipStream_t)stream : s->stream);
     if (!cx) return fail(PRT_ERR_OOM, "render context allocation failed");
     return enqueue_render(s, cx, cam, W, H, tw, th, tile_ids, n_tiles, spp, depth, seed, flags, d_out_sums, 0, false,
-                          n_frames, frame_stride);
+                          n_frames, frame_stride, out_pitch);
 }
 
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
@@ -1149,8 +1157,11 @@ int prt_render(void* scene, const float* cam, int W, int H, int x0, int y0, int 
     return PRT_OK;
 }
 
-int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_ids, int n_tiles, int tw, int th,
-                      int W, int H, float* d_frame, void* stream) {
+// shared by prt_scatter_tiles / prt_scatter_frames: argument checks and the (cached) upload of the
+// tile origins; then one scatter launch over n_tiles * tw * th slots
+static int scatter_enqueue(void* scene, const float* d_packed, const int32_t* tile_ids, int n_tiles, int tw, int th,
+                           int W, int H, int group_tiles, int64_t group_pitch, int n_frames, int64_t src_fpitch,
+                           float* d_frame, int64_t dst_fpitch, void* stream) {
     auto* s = (Scene*)scene;
     if (!s) return fail(PRT_ERR_ARG, "scene is NULL");
     if (n_tiles < 0 || (n_tiles > 0 && (!tile_ids || !d_packed || !d_frame))) return fail(PRT_ERR_ARG, "NULL argument");
@@ -1189,9 +1200,30 @@ int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_id
         HIP_TRY(hipStreamWaitEvent(st, s->scatter_ev, 0));
     }
     const int log_tw = __builtin_ctz((unsigned)tw), log_tpx = __builtin_ctz((unsigned)(tw * th));
-    HIP_TRY(prt::launch_scatter(d_packed, (const uint32_t*)s->scatter_xy.p, n_tiles * tw * th, log_tw, log_tpx, 0, 0, W,
-                                H, d_frame, st));
+    HIP_TRY(prt::launch_scatter_frames(d_packed, (const uint32_t*)s->scatter_xy.p, n_tiles * tw * th,
+                                       group_tiles * tw * th, group_pitch, n_frames, src_fpitch, dst_fpitch, log_tw,
+                                       log_tpx, 0, 0, W, H, d_frame, st));
     return PRT_OK;
+}
+
+int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_ids, int n_tiles, int tw, int th,
+                      int W, int H, float* d_frame, void* stream) {
+    return scatter_enqueue(scene, d_packed, tile_ids, n_tiles, tw, th, W, H, std::max(n_tiles, 1), 0, 1, 0, d_frame, 0,
+                           stream);
+}
+
+int prt_scatter_frames(void* scene, const float* d_packed, const int32_t* tile_ids, int n_groups, int group_tiles,
+                       int64_t group_pitch, int tw, int th, int W, int H, int n_frames, int64_t src_frame_pitch,
+                       float* d_frames, void* stream) {
+    if (n_groups < 0 || group_tiles < 1 || n_frames < 1 || n_frames > 65535)
+        return fail(PRT_ERR_ARG, "need n_groups >= 0, group_tiles >= 1 and 1 <= n_frames <= 65535");
+    const int64_t slot_f = (int64_t)tw * th * 3;
+    if (group_pitch < 0 || src_frame_pitch < 0 || (n_groups > 1 && group_pitch < group_tiles * slot_f) ||
+        (n_frames > 1 && src_frame_pitch < group_tiles * slot_f))
+        return fail(PRT_ERR_ARG, "group_pitch / src_frame_pitch must hold a group's tiles");
+    if ((int64_t)n_groups * group_tiles >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many tiles");
+    return scatter_enqueue(scene, d_packed, tile_ids, n_groups * group_tiles, tw, th, W, H, group_tiles, group_pitch,
+                           n_frames, src_frame_pitch, d_frames, 3 * (int64_t)W * H, stream);
 }
 
 int prt_render_multi(void* const* scenes, int n_scenes, const float* cam, int W, int H, int tile, int spp, int depth,

@@ -284,7 +284,18 @@ __device__ __forceinline__ bool sphere_hit(float4 sc, V3 o, V3 d, float t_min, f
 }
 
 // ---------------------------------------------------------------- traversal
-struct Counters { uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp, nonfinite, w_tri, q0, max_q; };
+struct Counters {
+    uint32_t nodes, tris, ext, shadow, it_inner, it_leaf, max_sp, nonfinite, w_tri, q0, max_q;
+    // STATS lane table (trace_kernel_pool, diag words 160..): wave-level trips of the traversal's
+    // inner-node and triangle loops, and the active lanes summed over those trips (wave_tick)
+    uint32_t wi, li, wl, ll;
+};
+// STATS: one wave-level trip of the enclosing loop body, booked by its first active lane, with
+// the lanes active in it: sum(l) / (64 sum(w)) is that loop's SIMD lane utilisation
+__device__ __forceinline__ void wave_tick(uint32_t& w, uint32_t& l) {
+    const uint32_t pc = (uint32_t)__popcll(__ballot(true));
+    if ((uint32_t)__builtin_amdgcn_readfirstlane(__lane_id()) == __lane_id()) { w += 1u; l += pc; }
+}
 
 // Moller-Trumbore in the reference's exact expression order
 // (intersection_taichi.py:69-91), for closest-hit and any-hit lanes of one wave.
@@ -564,6 +575,37 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     else step(stk);
 }
 
+// One inner-node visit over the LDS octant copy (visit_node4 OCT) for a lane whose query kind is
+// its own (trace_kernel_pool FUSED: a wave's lanes run closest-hit extension and any-hit shadow
+// queries side by side).  Closest-hit lanes take the first hit child of the octant's front-to-back
+// order and push the others; any-hit lanes see the children reversed, so they visit back to front
+// (MODE 2's order: a shadow ray ends at the light, where its occluders are likelier).  The kind
+// only permutes the four (ref, hit) pairs: four selects, then the closest-hit step.
+template <bool STATS>
+__device__ __forceinline__ void visit_oct_mixed(const float4* __restrict__ nodes, int& cur, int& sp, LdsStack16 st,
+                                                V3 inv, V3 oi, int sx, float tmin, float best, bool any,
+                                                Counters& cn) {
+    const float4* nd = nodes + (uint32_t)cur * 56u + sx;
+    const float4 nx = nd[0], fx = nd[1], ny = nd[2], fy = nd[3], nz = nd[4], fz = nd[5], rf = nd[6];
+    if (STATS) { cn.nodes++; cn.it_inner++; }
+    float t0, t1, t2, t3;
+    const bool h0 = slab_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, oi, inv, tmin, best, t0);
+    const bool h1 = slab_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, oi, inv, tmin, best, t1);
+    const bool h2 = slab_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, oi, inv, tmin, best, t2);
+    const bool h3 = slab_nf(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, oi, inv, tmin, best, t3);
+    const int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z), r3 = __float_as_int(rf.w);
+    const bool b0 = any ? h3 : h0, b1 = any ? h2 : h1, b2 = any ? h1 : h2, b3 = any ? h0 : h3;
+    const int a0 = any ? r3 : r0, a1 = any ? r2 : r1, a2 = any ? r1 : r2, a3 = any ? r0 : r3;
+    const bool p3 = b3 & (b0 | b1 | b2), p2 = b2 & (b0 | b1), p1 = b1 & b0;
+    st.put(sp + 1, a3); sp += p3 ? 1 : 0;
+    st.put(sp + 1, a2); sp += p2 ? 1 : 0;
+    st.put(sp + 1, a1); sp += p1 ? 1 : 0;
+    const int tp = st.get(sp);
+    const bool any_hit = b0 | b1 | b2 | b3;
+    cur = b0 ? a0 : (b1 ? a1 : (b2 ? a2 : (b3 ? a3 : tp)));
+    sp -= any_hit ? 0 : 1;
+}
+
 template <bool STATS, int MODE, class S, bool QN = false, bool RES = false, bool OCT = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
@@ -589,6 +631,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
     do {
         while (cur >= 0 && cur != S::kSent) {
             visit_node4<STATS, MODE, S, QN, OCT>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn, any);
+            if (STATS) wave_tick(cn.wi, cn.li);
             if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
@@ -614,7 +657,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
                 int id = __float_as_int(q0.w);
                 float t;
-                if (STATS) cn.tris++;
+                if (STATS) { cn.tris++; wave_tick(cn.wl, cn.ll); }
                 if (mt_u(xyz(q0), xyz(q1), xyz(q2), o, d, tmin, best, id, best_id, any, t)) {
                     best = t;
                     best_id = id;
@@ -873,7 +916,7 @@ void trace_kernel(TraceParams P) {
     V3 mis_n = v3(0, 0, 0), mis_n2 = v3(0, 0, 0), mis_fl = v3(0, 0, 0), mis_bd = v3(0, 0, 0);
     float mis_bp = 0.0f;
     float tmax = kTMax;
-    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t w_inner = 0, w_leaf = 0, l_inner = 0, l_leaf = 0;
     uint32_t chunk_s = 0;   // wave-uniform: sample index (within the launch) of the current chunk
     uint32_t chunk_xy0 = 0; // wave-uniform: origin of the current chunk's tile
@@ -1445,7 +1488,7 @@ __device__ __forceinline__ void copy_octant_nodes(float4* __restrict__ sn, const
 // octant BVH4 nodes, triangles, light triangles and offsets.  Shading data (normals, frames,
 // materials) are read from global memory (L1-resident) to keep seven blocks per CU.
 constexpr int kPoolF4 = 7 * kBlock / 4;        // pool SoA: 7 x 256 f32
-constexpr int kQueueF4 = kBlock / 16;          // queue: 256 u8
+constexpr int kQueueF4 = 2 * kBlock / 16;      // queue: 2 x 256 u8, by iteration parity
 constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 6, variant 9 all)
 #ifndef PRT_POOL_S_PRIO
 #define PRT_POOL_S_PRIO 2
@@ -1462,7 +1505,7 @@ constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 
 // PLAIN: the lean build for scenes without spheres and metal / dielectric materials (P.plain; C1, C2,
 // C5): without that code the kernel's loop keeps 17 fewer uniform values in spilled SGPRs and is a
 // third shorter
-template <bool STATS, int WPE, bool PLAIN>
+template <bool STATS, int WPE, bool PLAIN, bool FUSED>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel_pool(TraceParams P) {
     extern __shared__ float4 smem[];
@@ -1504,12 +1547,32 @@ void trace_kernel_pool(TraceParams P) {
     uint32_t st = 0;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0), wi = v3(0, 0, 0);
     V3 beta = v3(1, 1, 1), L = v3(0, 0, 0), pend = v3(0, 0, 0);
-    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t n_e = 0, n_s = 0, lanes_s = 0, pre_hits = 0;
+    // STATS lane table (diag words 160..175, tools/lane_table.py): (wave trips, lane trips) of E inner
+    // visits, E triangle tests, S inner visits, S triangle tests, the shading block, the Lambert
+    // block, the loop iteration (lanes busy after the refill) and the resolve of shadow answers
+    uint64_t lt[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // books a traversal's trip counters into lane-table entries k, k + 1 (inner) and k + 2, k + 3 (leaf)
+    auto book_trav = [&](int k) {
+        lt[k] += cn.wi; lt[k + 1] += cn.li; lt[k + 2] += cn.wl; lt[k + 3] += cn.ll;
+        cn.wi = 0; cn.li = 0; cn.wl = 0; cn.ll = 0;
+    };
+    auto book = [&](int k) {
+        uint32_t w = 0, l = 0;
+        wave_tick(w, l);
+        lt[k] += w; lt[k + 1] += l;
+    };
     uint32_t chunk_s = 0, chunk_xy0 = 0;
     // control words (kCtlF4): queue length [0..2], alive [3..5], chunk claims [6..8], S chunks done
     // [9..11], one triple entry per iteration mod 3 (a slot is reset two iterations after its use)
     uint32_t slot = 0, slot_prev = 0, nch_prev = 0;
+    // the queue's buffer (2 x 256 entries) alternates with the iteration's parity: entries enqueued in
+    // iteration i are read in i's S phase (FUSED: i + 1's traversal), and the next enqueue into the
+    // same buffer (iteration i + 2) comes after barrier i + 1, which every reader has passed
+    uint32_t qpar = 0, qpar_prev = 0;
+    // FUSED: rays in the previous iteration's queue, answered in this iteration's traversal
+    uint32_t nq_prev = 0;
 #ifdef PRT_POOL_CLOCKS
     // diagnostic build (tools/pool_clocks.py): wave-level cycles in E, at barrier 1, in S, at barrier 2
     uint64_t ck[6] = {0, 0, 0, 0, 0, 0};
@@ -1588,19 +1651,172 @@ void trace_kernel_pool(TraceParams P) {
         // ------------------------------------------------------------------ E phase
         refill();
         PRT_CLOCK(4);
+        if (STATS && item >= 0) book(12);
         // (a) extension traversal: every busy lane except one whose pending shadow ray ends its path
         const bool trav = item >= 0 && !(my_sh && bounce + 1 >= P.depth);
         int hid = -1;
         float ht = 0.0f;
         bool hit = false;
-        if (__ballot(trav) != 0) {
+        if constexpr (FUSED) {
+            // (a) FUSED: the lane's own extension query and the previous iteration's pooled shadow rays in
+            // ONE while-while loop.  A lane without a query (its extension query done, or none this
+            // iteration) claims the next queued shadow ray at the top of every inner + leaf round (one LDS
+            // atomic per wave) and traverses it any-hit, writing the answer into the owner's t_max word:
+            // the lanes that idled in the tail of the wave's extension traversals (lane table, round 5:
+            // inner visits at 44 %, triangle tests at 29 % of the lanes) run the shadow work, and no
+            // separate S phase follows the barrier.  The wave leaves once no lane holds a query and the
+            // queue has no unclaimed ray.  Answers do not depend on who traverses: images are
+            // bit-identical to the two-phase kernel's.
+            const uint32_t n_sq = nq_prev;
+            bool s_more = n_sq != 0u;   // wave-uniform: the previous queue may still hold unclaimed rays
+            bool e_act = trav, s_act = false, any = false;
+            int s_own = 0, cur = LdsStack16::kSent, leaf = 0, sp = 0, best_id = -1, sx = 0;
+            float best = kTMax;
+            V3 qo = o, qd = d, inv = v3(0, 0, 0), oi = v3(0, 0, 0);
+            auto q_init = [&](float tmax) {
+                inv = ray_inv(qd);
+                oi = qo * inv;
+                sx = 7 * ((__float_as_int(inv.x) < 0 ? 1 : 0) | (__float_as_int(inv.y) < 0 ? 2 : 0) |
+                          (__float_as_int(inv.z) < 0 ? 4 : 0));
+                stk.put(0, LdsStack16::kSent);
+                cur = root_for<LdsStack16>(tmax);
+                leaf = 0; sp = 0; best = tmax; best_id = -1;
+                if (STATS) cn.q0 = cn.nodes;
+            };
+            if (STATS && lane == __builtin_amdgcn_readfirstlane(lane) && __ballot(trav) != 0) n_e++;
+            if (trav) {
+                if (STATS) cn.ext++;
+                q_init(kTMax);
+            }
+            const int lb = exhausted ? 0 : P.leaf_break, le = exhausted ? 0 : P.leaf_exit;
+            uint32_t rounds = 0;
+            while (true) {
+                if (s_more) {
+                    const bool fr = !e_act && !s_act;
+                    const uint64_t m = __ballot(fr);
+                    if (m) {
+                        const uint32_t k = (uint32_t)__popcll(m);
+                        uint32_t base = 0;
+                        if (lane == __builtin_amdgcn_readfirstlane(lane)) base = atomicAdd(&ctl[6 + slot_prev], k);
+                        base = __builtin_amdgcn_readfirstlane(base);
+                        if (base + k >= n_sq) s_more = false;
+                        const uint32_t rank =
+                            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        if (fr && base + rank < n_sq) {
+                            s_own = queue[qpar_prev * kBlock + base + rank];
+                            qo = v3(pool[0 * kBlock + s_own], pool[1 * kBlock + s_own], pool[2 * kBlock + s_own]);
+                            qd = v3(pool[3 * kBlock + s_own], pool[4 * kBlock + s_own], pool[5 * kBlock + s_own]);
+                            any = true;
+                            s_act = true;
+                            q_init(pool[6 * kBlock + s_own]);
+                        }
+                    }
+                }
+                const bool act = e_act || s_act;
+                if (__ballot(act) == 0) break;
+                if (act) {
+                    // one round of traverse_ww4's while-while loop: descend until every descending lane
+                    // holds a leaf, then test leaves until at most `le` lanes still hold one
+                    while (cur >= 0 && cur != LdsStack16::kSent) {
+#ifdef PRT_FUSED_MIXED_ORDER
+                        // any-hit lanes back to front (per-lane selects: +18 VALU per visit, round 5)
+                        visit_oct_mixed<STATS>(g_nodes, cur, sp, stk, inv, oi, sx, kTMin, best, any, cn);
+#else
+                        // every lane front to back: the closest-hit visit without per-lane selects (an
+                        // any-hit query's answer does not depend on the order, only its visit count)
+                        visit_node4<STATS, 1, LdsStack16, false, true>(g_nodes, cur, sp, stk, inv, oi, sx, 0, 0, kTMin,
+                                                                       best, cn);
+#endif
+                        if (STATS) wave_tick(cn.wi, cn.li);
+                        if (cur < 0 && leaf >= 0) {
+                            leaf = cur;
+                            cur = stk.get(sp);
+                            --sp;
+                        }
+                        if (__popcll(__ballot(leaf >= 0)) <= (uint32_t)lb) break;
+                    }
+                    while (leaf < 0) {
+                        const int v = -leaf - 1;
+                        const int first = v >> 3, cnt = (v & 7) + 1;
+                        for (int k = 0; k < cnt; ++k) {
+                            const float4* tp = g_tris + (size_t)(first + k) * 3;
+                            const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+                            const int id = __float_as_int(q0.w);
+                            float t;
+                            if (STATS) { cn.tris++; wave_tick(cn.wl, cn.ll); }
+                            if (mt_u(xyz(q0), xyz(q1), xyz(q2), qo, qd, kTMin, best, id, best_id, any, t)) {
+                                best = t;
+                                best_id = id;
+                                if (any) { cur = LdsStack16::kSent; break; }
+                            }
+                        }
+                        if (any && best_id >= 0) { leaf = 0; break; }
+                        leaf = cur;
+                        if (cur < 0) {
+                            cur = stk.get(sp);
+                            --sp;
+                        }
+                        if (__popcll(__ballot(leaf < 0)) <= (uint32_t)le) break;
+                    }
+                }
+                // watchdog (traverse_ww4's): rounds of one iteration's loop, ends every query
+                if (++rounds > P.guard_trips) {
+                    if (lane == 0) atomicOr(P.fault, 1);
+                    cur = LdsStack16::kSent;
+                    leaf = 0;
+                    s_more = false;
+                }
+                const bool fin = act && cur == LdsStack16::kSent && leaf >= 0;
+                if (fin) {
+                    bool h = best_id >= 0;
+                    int bid = best_id;
+                    float bt = best;   // t_max when nothing was hit
+                    if (!PLAIN && P.n_sph > 0 && !(any && h)) {
+                        for (int k = 0; k < P.n_sph; ++k) {
+                            float root;
+                            if (sphere_hit(P.sph[k], qo, qd, kTMin, bt, root)) {
+                                bt = root;
+                                bid = P.n_tri + k;
+                                h = true;
+                                if (any) break;
+                            }
+                        }
+                    }
+                    if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
+                    if (s_act) {
+                        // the answer travels back in the owner's t_max word: NaN = occluded
+                        pool[6 * kBlock + s_own] = h ? __int_as_float(0x7FC00000) : 0.0f;
+                    } else {
+                        hid = h ? bid : -1;
+                        ht = bt;
+                        hit = h;
+                    }
+                }
+                const uint64_t ms = __ballot(fin && s_act);
+                if (fin) { e_act = false; s_act = false; }
+                if (ms) {
+                    if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) lanes_s += (uint64_t)__popcll(ms);
+                    // publish the answers before counting them
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    if (lane == __builtin_amdgcn_readfirstlane(lane))
+                        __hip_atomic_fetch_add(&ctl[9 + slot_prev], (uint32_t)__popcll(ms), __ATOMIC_RELEASE,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_s++;
+            }
+            if (STATS) book_trav(0);
+            // the own extension ray again: origin from the pool slot, direction wi (neither stayed in
+            // registers across the shadow queries this lane ran)
+            o = v3(pool[0 * kBlock + tid], pool[1 * kBlock + tid], pool[2 * kBlock + tid]);
+            d = wi;
+        } else if (__ballot(trav) != 0) {
             if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_e++;
             if (trav) {
                 if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
                 hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
                     g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
+                if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
                 if (!PLAIN && P.n_sph > 0) {
                     float best = hit ? ht : kTMax;
                     for (int k = 0; k < P.n_sph; ++k) {
@@ -1616,23 +1832,33 @@ void trace_kernel_pool(TraceParams P) {
             }
         }
         PRT_CLOCK(5);
-        // (b) the previous S phase's answers (its waves ran it beside this wave's traversal): a wave
-        // with a pending shadow ray waits until every chunk of that phase has been answered
+        // (b) the previous S phase's answers (its waves ran it beside this wave's traversal; FUSED: the
+        // block's traversals of this iteration): a wave with a pending shadow ray waits until every
+        // chunk (FUSED: every ray) of the previous queue has been answered
         if (__ballot(my_sh) != 0) {
             // bounded: a wait that never ends (a logic error) raises the watchdog flag instead of
-            // hanging the device (2^20 sleeps of 64 clocks ~ 30 ms)
-            for (uint32_t spin = 0; nch_prev &&
-                 __hip_atomic_load(&ctl[9 + slot_prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < nch_prev;
+            // hanging the device: 2^20 sleeps of 64 clocks ~ 30 ms, against a worst case of ~0.1 ms for
+            // the answers (an LDS scene is <= 24 KiB: a query visits each of its <= ~100 nodes and
+            // <= ~500 triangles at most once, ~10^5 cycles even in a STATS build).  A lane whose answer
+            // did not arrive ends with NaN radiance (counted by STATS' non-finite samples), so a tripped
+            // wait cannot pass for a valid image even before prt_check_faults reports it.
+            const uint32_t need = FUSED ? nq_prev : nch_prev;
+            bool late = false;
+            for (uint32_t spin = 0;
+                 need && __hip_atomic_load(&ctl[9 + slot_prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need;
                  ++spin) {
                 if (spin >= (1u << 20)) {
                     if (lane == 0) atomicOr(P.fault, 2);
+                    late = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
             if (my_sh) {
+                if (STATS) book(14);
                 const float r = pool[6 * kBlock + tid];
-                if (r == r) L = L + pend;   // not occluded
+                if (late) L = v3(__int_as_float(0x7FC00000), __int_as_float(0x7FC00000), __int_as_float(0x7FC00000));
+                else if (r == r) L = L + pend;   // not occluded
                 my_sh = false;
                 ++bounce;
                 if (bounce >= P.depth) {
@@ -1645,6 +1871,7 @@ void trace_kernel_pool(TraceParams P) {
         }
         // (c) shading of this iteration's extension hits
         if (trav) {
+            if (STATS) book(8);
             {
                 bool finished = false;
                 if (!hit) {
@@ -1701,6 +1928,7 @@ void trace_kernel_pool(TraceParams P) {
                         }
                         finished = true;
                     } else {
+                        if (STATS) book(10);
                         float u0 = rng_next(st);
                         float u1 = rng_next(st);
                         V3 l = cosine_hemisphere<true>(u0, u1);
@@ -1784,7 +2012,7 @@ void trace_kernel_pool(TraceParams P) {
                 if (lane == __builtin_amdgcn_readfirstlane(lane)) base = atomicAdd(&ctl[slot], cnt);
                 base = __builtin_amdgcn_readfirstlane(base);
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                if (my_sh) queue[base + rank] = (uint8_t)tid;
+                if (my_sh) queue[qpar * kBlock + base + rank] = (uint8_t)tid;
             }
             // a wave with busy lanes or unclaimed work keeps the block looping
             if ((__ballot(item >= 0) != 0 || !exhausted) && lane == 0) ctl[3 + slot] = 1u;
@@ -1799,6 +2027,10 @@ void trace_kernel_pool(TraceParams P) {
         PRT_CLOCK(1);
         // ------------------------------------------------------------------ S phase
         const uint32_t n_q = ctl[slot];
+        if constexpr (FUSED) {
+            // no S phase: the next iteration's traversals answer this queue
+            nq_prev = n_q;
+        } else {
         // the queue's rays in ceil(n / 64) chunks, one to each of the first waves to claim one (<= 4
         // chunks, one claim per wave); the others refill the lanes that finished in E meanwhile,
         // off the critical path
@@ -1818,7 +2050,7 @@ void trace_kernel_pool(TraceParams P) {
             const uint32_t e = e0 + (uint32_t)lane;
             if (STATS && lane == 0) { n_s++; lanes_s += e1 - e0; }
             if (e < e1) {
-                const int owner = queue[e];
+                const int owner = queue[qpar * kBlock + e];
                 const V3 so = v3(pool[0 * kBlock + owner], pool[1 * kBlock + owner], pool[2 * kBlock + owner]);
                 const V3 sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
                 const float stm = pool[6 * kBlock + owner];
@@ -1828,7 +2060,7 @@ void trace_kernel_pool(TraceParams P) {
                 bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
                     g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
+                if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
                 if (!PLAIN && P.n_sph > 0 && !hit) {
                     for (int k = 0; k < P.n_sph; ++k) {
                         float root;
@@ -1843,11 +2075,14 @@ void trace_kernel_pool(TraceParams P) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_fetch_add(&ctl[9 + slot], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        nch_prev = n_chunks;
+        }   // !FUSED
         PRT_CLOCK(2);
         const bool alive = ctl[3 + slot] != 0u;
-        nch_prev = n_chunks;
         slot_prev = slot;
         slot = slot == 2 ? 0u : slot + 1u;
+        qpar_prev = qpar;
+        qpar ^= 1u;
         // the next extension ray: origin from the pool slot, direction wi (no register keeps the
         // previous ray across the S phase, where the lane may traverse another lane's ray)
         o = v3(pool[0 * kBlock + tid], pool[1 * kBlock + tid], pool[2 * kBlock + tid]);
@@ -1877,6 +2112,11 @@ void trace_kernel_pool(TraceParams P) {
             // iterations, shadow rays answered by the light-triangle test
             for (int k = 0; k < 4; ++k) atomicAdd(P.stats + 17 + k, (unsigned long long)ph[k]);
         }
+        for (int k = 0; k < 16; ++k) {
+            uint64_t v = lt[k];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+            if (lane == 0 && v) atomicAdd(P.stats + 160 + k, (unsigned long long)v);
+        }
         uint32_t msp = cn.max_sp, nf = cn.nonfinite, mq = cn.max_q;
         for (int off = 32; off > 0; off >>= 1) {
             msp = max(msp, (uint32_t)__shfl_down((int)msp, off));
@@ -1894,7 +2134,7 @@ void trace_kernel_pool(TraceParams P) {
 }  // namespace
 
 // variant table: (VAR bits of trace_kernel, LDS-resident scene, min waves per SIMD); see prt_kernels.h
-// (bit 512: the block-pooled shadow-query kernel trace_kernel_pool)
+// (bit 512: the block-pooled shadow-query kernel trace_kernel_pool; bit 1024: its FUSED schedule)
 #define PRT_VARIANTS(X)                       \
     X(kVarLds, 8, true, 7)                    \
     X(kVarLdsAnyOcc, 8, true, 1)              \
@@ -1903,7 +2143,9 @@ void trace_kernel_pool(TraceParams P) {
     X(kVarLds6, 8, true, 6)                   \
     X(kVarGlobalMis, 480, false, 6)           \
     X(kVarLdsPool, 512, true, 7)              \
-    X(kVarLdsPool6, 512, true, 6)
+    X(kVarLdsPool6, 512, true, 6)             \
+    X(kVarLdsFused, 1536, true, 7)            \
+    X(kVarLdsFused6, 1536, true, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
@@ -1912,7 +2154,7 @@ static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStr
     if constexpr ((VAR & 512) != 0) {
         // the pool kernel's LDS stack size is a launch parameter (P.lds_stack): one instantiation,
         // compiled in its own unit (prt_trace_pool.hip, other register-allocation flags)
-        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, grid, smem, stream);
+        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, (VAR & 1024) != 0, grid, smem, stream);
         else return hipErrorInvalidValue;
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
         trace_kernel<STACK, STATS, VAR, LDS, WPE><<<grid, kBlock, smem, stream>>>(P);
@@ -1937,7 +2179,7 @@ template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
 static void occ_one(int* n, size_t smem) {
     constexpr bool spill = (VAR & 32) != 0;
     if constexpr ((VAR & 512) != 0) {
-        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, smem);
+        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, (VAR & 1024) != 0, smem);
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(n, trace_kernel<STACK, STATS, VAR, LDS, WPE>, kBlock, smem);
 }

@@ -78,8 +78,11 @@ constexpr int kVarLds6 = 6;        // kVarLds built for >= 6 waves/SIMD (80 VGPR
 constexpr int kVarLdsPool = 7;     // LDS-resident scene, block-pooled shadow queries (trace_kernel_pool),
                                    // >= 7 waves/SIMD; the LDS stack size is P.lds_stack
 constexpr int kVarLdsPool6 = 8;    // kVarLdsPool built for >= 6 waves/SIMD (80 VGPRs)
+constexpr int kVarLdsFused = 9;    // trace_kernel_pool FUSED (round 5): the extension traversals' idle lanes
+                                   // answer the previous iteration's pooled shadow rays; no S phase
+constexpr int kVarLdsFused6 = 10;  // kVarLdsFused built for >= 6 waves/SIMD
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 8;
+constexpr int kVarLast = 10;
 bool variant_pool(int var);
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
@@ -103,16 +106,23 @@ hipError_t launch_rays_prep(const TraceParams& P, const float* in8, int64_t n, i
 size_t lds_scene_bytes(const TraceParams& P);  // LDS-resident scene + shading data
 hipError_t launch_trace(const TraceParams& P, int stack, int var, int grid, bool stats, hipStream_t stream);
 // per-frame sample-order sums of one chunk of launch samples [j0, j0 + n): frames f0 .. f0 + n_frames - 1
-// (frame f = launch samples [f spp, (f + 1) spp)) into acc + f n_slots 3, in one launch
+// (frame f = launch samples [f spp, (f + 1) spp)) into acc + f pitch (floats, >= 3 n_slots), in one launch
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int64_t j0, int64_t n, int64_t spp, int64_t f0,
-                         int64_t n_frames, bool accumulate, hipStream_t stream);
+                         int64_t n_frames, int64_t pitch, bool accumulate, hipStream_t stream);
 // packed tile slots (tile origins tile_xy) -> [x][y] window of the frame (prt_render, prt_render_multi)
 hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_slots, int log_tw, int log_tpx, int x0,
                           int y0, int w, int h, float* out, hipStream_t stream);
+// grouped slots (group g at packed + g group_pitch floats, group_slots slots each) of n_frames frames
+// (source frame f at + f src_fpitch, output frame f at out + f dst_fpitch), one launch
+hipError_t launch_scatter_frames(const float* packed, const uint32_t* tile_xy, int n_slots, int group_slots,
+                                 int64_t group_pitch, int n_frames, int64_t src_fpitch, int64_t dst_fpitch, int log_tw,
+                                 int log_tpx, int x0, int y0, int w, int h, float* out, hipStream_t stream);
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 // the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
 // the pooled kernel's lean instantiation (no sphere or specular code) runs when P.plain is set
-hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream);
-int trace_occ_pool(bool stats, int wpe, size_t smem);
+// (fused: the schedule whose extension traversals also answer the previous iteration's shadow rays)
+hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, bool fused, int grid, size_t smem,
+                             hipStream_t stream);
+int trace_occ_pool(bool stats, int wpe, bool fused, size_t smem);
 
 }  // namespace prt

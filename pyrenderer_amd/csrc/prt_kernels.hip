@@ -80,7 +80,7 @@ __global__ __launch_bounds__(kBlock) void hits_kernel(TraceParams P, const float
     if (i >= n) return;
     float4 a = rays[2 * i], b = rays[2 * i + 1];
     V3 o = v3(a.x, a.y, a.z), d = v3(b.x, b.y, b.z);
-    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Counters cn = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     int hid = -1;
     float ht = 0.0f;
     bool hit = traverse_ww4<false, ANY ? 2 : 1, LdsStack, QN>(P.nodes, P.tris, o, d, a.w, b.w, ANY, stk, hid, ht, cn,
@@ -185,10 +185,14 @@ __global__ __launch_bounds__(kBlock) void rays_prep_kernel(TraceParams P, const 
 // tile_xy = (x0 << 16) | y0 per tile (the trace kernel's tile origins); slots outside the
 // window (ragged frame edges, tiles straddling the window) are dropped.  Used by
 // prt_render (one window) and prt_render_multi (each rank's gathered tiles into the frame).
+// Grouped / multi-frame form (prt_scatter_frames): the slots come in groups of `group_slots`
+// (one rank's gather block), group g at packed + g * group_pitch floats; frame f = blockIdx.y reads
+// at + f * src_fpitch and writes out + f * dst_fpitch (one launch for every frame of a gather)
 __global__ __launch_bounds__(kBlock) void scatter_kernel(const float* __restrict__ packed,
                                                          const uint32_t* __restrict__ tile_xy, int n_slots,
-                                                         int log_tw, int log_tpx, int x0, int y0, int w, int h,
-                                                         float* __restrict__ out) {
+                                                         int group_slots, int64_t group_pitch, int64_t src_fpitch,
+                                                         int64_t dst_fpitch, int log_tw, int log_tpx, int x0, int y0,
+                                                         int w, int h, float* __restrict__ out) {
     int slot = blockIdx.x * kBlock + threadIdx.x;
     if (slot >= n_slots) return;
     uint32_t xy = tile_xy[slot >> log_tpx];
@@ -196,19 +200,21 @@ __global__ __launch_bounds__(kBlock) void scatter_kernel(const float* __restrict
     int x = (int)(xy >> 16) + (r & ((1 << log_tw) - 1)) - x0;
     int y = (int)(xy & 0xFFFFu) + (r >> log_tw) - y0;
     if (x < 0 || y < 0 || x >= w || y >= h) return;
-    const float* p = packed + 3 * (size_t)slot;
-    float* o = out + ((size_t)x * h + y) * 3;
+    const int g = slot / group_slots;
+    const float* p = packed + (size_t)g * group_pitch + 3 * (size_t)(slot - g * group_slots) +
+                     (size_t)blockIdx.y * src_fpitch;
+    float* o = out + (size_t)blockIdx.y * dst_fpitch + ((size_t)x * h + y) * 3;
     o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
 }
 
 // Sequential per-pixel sum over this chunk's samples, in sample order, onto
 // the running sums (bit-identical to acc = acc + L[s] for s = 0..spp-1).  One launch covers every
 // frame the chunk touches (blockIdx.y): frame f = f0 + y owns the chunk's launch samples
-// [max(j0, f spp), min(j0 + n, (f + 1) spp)), summed into acc + f n_slots 3; a frame's first
-// samples start its sums (unless accumulating), later chunks continue them.
+// [max(j0, f spp), min(j0 + n, (f + 1) spp)), summed into acc + f pitch (pitch >= 3 n_slots floats); a
+// frame's first samples start its sums (unless accumulating), later chunks continue them.
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict__ buf, float* __restrict__ acc0,
                                                         int n_slots, int64_t j0, int64_t n, int64_t spp, int64_t f0,
-                                                        int accumulate) {
+                                                        int64_t pitch, int accumulate) {
     int slot = blockIdx.x * kBlock + threadIdx.x;
     if (slot >= n_slots) return;
     const int64_t f = f0 + blockIdx.y;
@@ -216,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const float* __restrict_
     const int n_spp = (int)(e - a);
     const int first = (a == f * spp) && !accumulate;
     buf += (size_t)(a - j0) * n_slots * 3;
-    float* __restrict__ acc = acc0 + (size_t)f * n_slots * 3;
+    float* __restrict__ acc = acc0 + (size_t)f * (size_t)pitch;
     float r = 0.0f, g = 0.0f, b = 0.0f;
     if (!first) { r = acc[3 * (size_t)slot]; g = acc[3 * (size_t)slot + 1]; b = acc[3 * (size_t)slot + 2]; }
     for (int s = 0; s < n_spp; ++s) {
@@ -297,9 +303,18 @@ hipError_t launch_rays_prep(const TraceParams& P, const float* in8, int64_t n, i
 
 hipError_t launch_scatter(const float* packed, const uint32_t* tile_xy, int n_slots, int log_tw, int log_tpx, int x0,
                           int y0, int w, int h, float* out, hipStream_t stream) {
-    if (n_slots <= 0) return hipSuccess;
-    scatter_kernel<<<(n_slots + kBlock - 1) / kBlock, kBlock, 0, stream>>>(packed, tile_xy, n_slots, log_tw, log_tpx,
-                                                                           x0, y0, w, h, out);
+    return launch_scatter_frames(packed, tile_xy, n_slots, n_slots, 0, 1, 0, 0, log_tw, log_tpx, x0, y0, w, h, out,
+                                 stream);
+}
+
+hipError_t launch_scatter_frames(const float* packed, const uint32_t* tile_xy, int n_slots, int group_slots,
+                                 int64_t group_pitch, int n_frames, int64_t src_fpitch, int64_t dst_fpitch, int log_tw,
+                                 int log_tpx, int x0, int y0, int w, int h, float* out, hipStream_t stream) {
+    if (n_slots <= 0 || n_frames <= 0) return hipSuccess;
+    if (group_slots <= 0 || n_frames > 65535) return hipErrorInvalidValue;
+    dim3 grid((unsigned)((n_slots + kBlock - 1) / kBlock), (unsigned)n_frames);
+    scatter_kernel<<<grid, kBlock, 0, stream>>>(packed, tile_xy, n_slots, group_slots, group_pitch, src_fpitch,
+                                                dst_fpitch, log_tw, log_tpx, x0, y0, w, h, out);
     return hipGetLastError();
 }
 
@@ -310,10 +325,10 @@ hipError_t launch_camera(const TraceParams& P, float4* rays, float4* ray_o, hipS
 }
 
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int64_t j0, int64_t n, int64_t spp, int64_t f0,
-                         int64_t n_frames, bool accumulate, hipStream_t stream) {
-    if (n_frames <= 0 || n_frames > 65535) return hipErrorInvalidValue;
+                         int64_t n_frames, int64_t pitch, bool accumulate, hipStream_t stream) {
+    if (n_frames <= 0 || n_frames > 65535 || pitch < 3 * (int64_t)n_slots) return hipErrorInvalidValue;
     dim3 grid((unsigned)((n_slots + kBlock - 1) / kBlock), (unsigned)n_frames);
-    reduce_kernel<<<grid, kBlock, 0, stream>>>(buf, acc, n_slots, j0, n, spp, f0, accumulate ? 1 : 0);
+    reduce_kernel<<<grid, kBlock, 0, stream>>>(buf, acc, n_slots, j0, n, spp, f0, pitch, accumulate ? 1 : 0);
     return hipGetLastError();
 }
 

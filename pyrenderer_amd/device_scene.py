@@ -150,14 +150,15 @@ class DeviceScene:
                                                 ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def render_frames_device(self, cam, W, H, tw, th, tile_ids, spp, depth, n_frames, d_out_ptr, stream_ptr=None,
-                             seed=0, frame_stride=0, flags=0):
+                             seed=0, frame_stride=0, flags=0, out_pitch=0):
         """prt_render_frames_device: n_frames frames through the same persistent launches; frame f
-        (samples f * frame_stride + 0..spp-1) -> d_out_ptr + f * n_slots * 3 floats.  Enqueued."""
+        (samples f * frame_stride + 0..spp-1) -> d_out_ptr + f * out_pitch floats (0: packed,
+        n_slots * 3 floats).  Enqueued."""
         cam = np.ascontiguousarray(cam, np.float32)
         tile_ids = np.ascontiguousarray(tile_ids, np.int32)
         N.check(N.lib().prt_render_frames_device(self.h, N.ptr(cam), W, H, tw, th, N.ptr(tile_ids),
                                                  tile_ids.shape[0], spp, depth, int(seed), int(n_frames),
-                                                 int(frame_stride), flags, ctypes.c_void_p(d_out_ptr),
+                                                 int(frame_stride), flags, ctypes.c_void_p(d_out_ptr), int(out_pitch),
                                                  ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def scatter_tiles(self, d_packed_ptr, tile_ids, tw, th, W, H, d_frame_ptr, stream_ptr=None):
@@ -166,6 +167,19 @@ class DeviceScene:
         N.check(N.lib().prt_scatter_tiles(self.h, ctypes.c_void_p(d_packed_ptr), N.ptr(tile_ids), tile_ids.shape[0],
                                           tw, th, W, H, ctypes.c_void_p(d_frame_ptr),
                                           ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def scatter_frames(self, d_packed_ptr, tile_ids, group_tiles, group_pitch, tw, th, W, H, n_frames, src_frame_pitch,
+                       d_frames_ptr, stream_ptr=None):
+        """prt_scatter_frames: a rank-major gather buffer of n_frames frames (rank r's block at
+        d_packed + r * group_pitch floats, frame f at + f * src_frame_pitch) -> the device frames
+        (n_frames, W, H, 3), one launch.  tile_ids: n_groups * group_tiles host ids, -1 = padding."""
+        tile_ids = np.ascontiguousarray(tile_ids, np.int32)
+        if tile_ids.shape[0] % group_tiles:
+            raise ValueError("tile_ids must hold whole groups of group_tiles ids")
+        N.check(N.lib().prt_scatter_frames(self.h, ctypes.c_void_p(d_packed_ptr), N.ptr(tile_ids),
+                                           tile_ids.shape[0] // group_tiles, group_tiles, int(group_pitch), tw, th, W,
+                                           H, int(n_frames), int(src_frame_pitch), ctypes.c_void_p(d_frames_ptr),
+                                           ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
     def closest_hits(self, o, d, tmin, tmax, any_hit=False, quantized=False):
         """World.hit_all on the GPU for arrays of rays: (hit_id, t); id -1 = miss."""

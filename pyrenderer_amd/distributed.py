@@ -35,6 +35,9 @@ class TileShard:
         self.slot_elems = tile * tile * 3
         self.bufs = torch.zeros((self.frames, self.max_tiles * self.slot_elems), dtype=torch.float32, device=device)
         self.buf = self.bufs[0]
+        # floats between consecutive frames of `bufs` (the largest shard's slot, >= this rank's tiles):
+        # the out_pitch of DeviceScene.render_frames_device into bufs
+        self.pitch = int(self.bufs.shape[1])
         self.host_staging = bool(host_staging) and self.buf.is_cuda
         self.wire = torch.empty_like(self.bufs, device="cpu") if self.host_staging else self.bufs
         self.gathered = None
@@ -45,12 +48,12 @@ class TileShard:
             self.gathered = torch.empty((world, self.frames, self.bufs.shape[1]), dtype=torch.float32,
                                         device=self.wire.device)
         self.per_rank = [interleaved_tiles(W, H, tile, r, world, scheme) for r in range(world)]
-        # scatter tile list seen from frame f's base: rank r's tile t at position (r * frames) *
-        # max_tiles + t, every other position (other frames' tiles, padding) id -1 (dropped)
-        ids = np.full((world, self.frames, self.max_tiles), -1, np.int32)
+        # rank-major tile ids of the gather buffer, max_tiles per rank (padding id -1, dropped): the
+        # scatter reads rank r's block at r * frames * pitch floats (prt_scatter_frames)
+        ids = np.full((world, self.max_tiles), -1, np.int32)
         for r, t in enumerate(self.per_rank):
-            ids[r, 0, :len(t)] = t
-        self.scatter_ids = ids.reshape(-1)[:((world - 1) * self.frames + 1) * self.max_tiles]
+            ids[r, :len(t)] = t
+        self.scatter_ids = ids.reshape(-1)
         self.frame_out = None    # rank 0's device frames (frames, W, H, 3), allocated by scatter()
         self.packed_dev = None   # gloo: the gathered host buffer's device copy
 
@@ -73,12 +76,37 @@ class TileShard:
     def frame(self):
         return None if self.frame_out is None else self.frame_out[0]
 
+    def scatter_frames(self, device_scene, stream=None, n_frames=1):
+        """Rank 0 after gather(n_frames): every rank's tiles of frames 0 .. n_frames-1 -> the device
+        frames frame_out[:n_frames], ONE launch (prt_scatter_frames over world x max_tiles slots per
+        frame, ADVICE r04: not (world - 1) x frames of other frames' padding), enqueued on `stream`.
+        This is the root-side step of SURVEY.md §8(e) that bench.py times inside every N > 1 step."""
+        dev = torch.device("cuda", device_scene.device)
+        s = stream or torch.cuda.current_stream(dev)
+        with torch.cuda.stream(s):
+            if self.frame_out is None:
+                self.frame_out = torch.zeros((self.frames, self.W, self.H, 3), dtype=torch.float32, device=dev)
+            if self.world == 1:
+                packed, ids, group_pitch = self.bufs, self.per_rank[0], 0
+            else:
+                packed = self.gathered
+                if not packed.is_cuda:
+                    if self.packed_dev is None:
+                        self.packed_dev = torch.empty_like(self.gathered, device=dev)
+                    self.packed_dev.copy_(self.gathered)
+                    packed = self.packed_dev
+                ids, group_pitch = self.scatter_ids, self.frames * self.pitch
+        group_tiles = self.max_tiles if self.world > 1 else max(len(ids), 1)
+        if len(ids):
+            device_scene.scatter_frames(packed.data_ptr(), ids, group_tiles, group_pitch, self.tile, self.tile, self.W,
+                                        self.H, n_frames, self.pitch, self.frame_out.data_ptr(), s.cuda_stream)
+        return self.frame_out[:n_frames]
+
     def scatter(self, device_scene, stream=None, f=0):
         """Rank 0 after gather(): every rank's tiles of frame f -> the (W, H, 3) device frame
-        `frame_out[f]` by libprt's scatter kernel (prt_scatter_tiles, one launch over the gathered
-        buffer from frame f's base), enqueued on `stream` (default: torch's current stream).
-        gloo's host buffer is first uploaded on that stream (once per group, with frame 0).  This is
-        the root-side step of SURVEY.md §8(e) that bench.py times inside every N > 1 step."""
+        `frame_out[f]` (one prt_scatter_frames launch from frame f's base), enqueued on `stream`
+        (default: torch's current stream).  gloo's host buffer is first uploaded on that stream (once
+        per group, with frame 0)."""
         dev = torch.device("cuda", device_scene.device)
         s = stream or torch.cuda.current_stream(dev)
         with torch.cuda.stream(s):
@@ -87,7 +115,7 @@ class TileShard:
             if self.frame_out is None:
                 self.frame_out = torch.zeros((self.frames, self.W, self.H, 3), dtype=torch.float32, device=dev)
             if self.world == 1:
-                base = self.bufs[f]
+                base, ids, group_pitch = self.bufs[f], self.per_rank[0], 0
             else:
                 packed = self.gathered
                 if not packed.is_cuda:
@@ -96,10 +124,11 @@ class TileShard:
                     if f == 0:
                         self.packed_dev.copy_(self.gathered)
                     packed = self.packed_dev
-                base = packed[0, f]
-        ids = self.scatter_ids if self.world > 1 else self.per_rank[0]
-        device_scene.scatter_tiles(base.data_ptr(), ids, self.tile, self.tile, self.W, self.H,
-                                   self.frame_out[f].data_ptr(), s.cuda_stream)
+                base, ids, group_pitch = packed[0, f], self.scatter_ids, self.frames * self.pitch
+        group_tiles = self.max_tiles if self.world > 1 else max(len(ids), 1)
+        if len(ids):
+            device_scene.scatter_frames(base.data_ptr(), ids, group_tiles, group_pitch, self.tile, self.tile, self.W,
+                                        self.H, 1, self.pitch, self.frame_out[f].data_ptr(), s.cuda_stream)
         return self.frame_out[f]
 
     def assemble(self, device_scene=None, stream=None, f=0):

@@ -22,7 +22,7 @@ def test_library_exports_header_symbols():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(N.EXPORTS), set(names) ^ set(N.EXPORTS)
-    assert L.prt_abi_version() == N.ABI_VERSION == 2
+    assert L.prt_abi_version() == N.ABI_VERSION == 3
 
 
 def test_device_count_without_gpu_is_ok():

@@ -73,10 +73,44 @@ def test_frames_argument_checks(gpu_scene, cornell):
     from pyrenderer_amd._native import PrtError
     scene, cam, flat = cornell
     packed = cam.convert_to_taichi_camera().packed()
-    out = torch.zeros(64 * 3, dtype=torch.float32, device="cuda:0")
-    for n, stride in ((0, 0), (2, -1)):
+    out = torch.zeros(2 * 64 * 3, dtype=torch.float32, device="cuda:0")
+    for n, stride, pitch in ((0, 0, 0), (2, -1, 0), (2, 1, 64 * 3 - 1)):
         with pytest.raises(PrtError):
-            gpu_scene.render_frames_device(packed, 8, 8, 8, 8, [0], 1, 1, n, out.data_ptr(), frame_stride=stride)
+            gpu_scene.render_frames_device(packed, 8, 8, 8, 8, [0], 1, 1, n, out.data_ptr(), frame_stride=stride,
+                                           out_pitch=pitch)
+
+
+@pytest.mark.parametrize("world", [3, 5])
+def test_ragged_shard_frames_land_in_their_gather_rows(gpu_scene, cornell, oracle_scene, world):
+    """a rank owning fewer tiles than the gather slot (max_tiles) renders F > 1
+    frames straight into TileShard.bufs at the slot's pitch (bench.py's call): every frame f sits in
+    row f, equal to the render of its own samples, and the padding after the rank's tiles is untouched."""
+    import torch
+    from pyrenderer_amd.distributed import TileShard
+    scene, cam, flat = cornell
+    packed = cam.convert_to_taichi_camera().packed()
+    W = H = 128
+    tile, spp, depth, F, seed = 16, 4, 4, 4, 5
+    sh = None
+    for r in range(world):
+        s = TileShard(W, H, tile, r, world, torch.device("cuda", 0), frames=F)
+        if len(s.tiles) < s.max_tiles:
+            sh = s
+            break
+    assert sh is not None, "no ragged rank"
+    sh.bufs.fill_(float("nan"))
+    n = len(sh.tiles) * tile * tile * 3
+    gpu_scene.render_frames_device(packed, W, H, tile, tile, sh.tiles, spp, depth, F, sh.bufs.data_ptr(), None,
+                                   seed=seed, frame_stride=spp, out_pitch=sh.pitch)
+    gpu_scene.check_faults()
+    bufs = sh.bufs.cpu().numpy()
+    for f in range(F):
+        ref = np.zeros((len(sh.tiles) * tile * tile, 3), np.float32)
+        gpu_scene.render_tiles_accumulate(packed, W, H, tile, tile, sh.tiles, f * spp, spp, depth, ref, seed=seed)
+        assert np.array_equal(bufs[f, :n].reshape(-1, 3), ref), f
+        assert np.isnan(bufs[f, n:]).all(), f          # the slot's padding is not written
+    cpu = oracle_scene.render_tiles(packed, W, H, tile, tile, sh.tiles[:2], spp, depth, seed=seed)
+    assert np.array_equal(bufs[0, :2 * tile * tile * 3].reshape(-1, 3), cpu)
 
 
 def test_in_kernel_camera_flag_is_rejected(gpu_scene, cornell):

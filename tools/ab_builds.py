@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=6)
+    ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant for every library (0 = default)")
     a = ap.parse_args()
     import torch
 
@@ -64,12 +65,12 @@ def main():
             # one untimed launch first: the device idled during the previous library's host-side
             # compare, and the first launch after an idle gap runs at a lower clock
             ds.render_tiles_device(cam, W, H, 64, 64, ids, cfg["spp"], cfg["depth"], buf.data_ptr(),
-                                   stream.cuda_stream, flags=N.PRT_FLAG_TIME)
+                                   stream.cuda_stream, flags=N.PRT_FLAG_TIME | (a.variant << 8))
             torch.cuda.synchronize(dev)
             ds.kernel_timing()
             for _ in range(a.launches):
                 ds.render_tiles_device(cam, W, H, 64, 64, ids, cfg["spp"], cfg["depth"], buf.data_ptr(),
-                                       stream.cuda_stream, flags=N.PRT_FLAG_TIME)
+                                       stream.cuda_stream, flags=N.PRT_FLAG_TIME | (a.variant << 8))
             torch.cuda.synchronize(dev)
             ms, n = ds.kernel_timing()
             out = buf.cpu().numpy()

@@ -73,7 +73,7 @@ def main():
         ds.render_tiles(c, W, H, 64, 64, ids, a.spp, a.depth, 0, PRT_FLAG_STATS | vflags(v))
         dg = ds.diag_words(22).astype(np.float64)   # 17..21: ext / shadow iteration clocks, counts, lanes
         tot = dg[4] + dg[5] + dg[6]
-        if v.rstrip("np") in ("7", "8"):
+        if v.rstrip("np") in ("7", "8", "9", "10"):
             # trace_kernel_pool's diag words 17..20: wave E iterations, wave S iterations, lanes of the
             # S iterations, shadow rays answered by the light-triangle test
             print(json.dumps({"variant": v, "pool": {
