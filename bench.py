@@ -102,6 +102,10 @@ def parse():
                     help="torch.distributed backend for N > 1: nccl (= RCCL over xGMI, the default) or gloo "
                          "(tile sums staged through host memory; rehearses the N > 1 path with several ranks "
                          "on one GPU)")
+    ap.add_argument("--single-frame-steps", type=int, default=5,
+                    help="extra timed leg after the main one: this many steps of ONE frame per launch (what a "
+                         "caller's one-shot render of one frame costs), reported as `single_frame`; 0 = skip "
+                         "(also skipped when the main leg already runs one frame per launch)")
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant id (0 = the library's default)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU time of the baseline sample")
@@ -278,6 +282,35 @@ def launch_check(args, env=None):
     return None
 
 
+def rank_identity(dev, rank=0, local_rank=0):
+    """This rank's GPU, as the line reports it (config.ranks): rank, local rank, torch device index,
+    the device's PCI address (domain:bus:device) and UUID — what makes an N-GPU line self-proving
+    (N distinct PCI addresses = N distinct GPUs rendered)."""
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    return {"rank": int(rank), "local_rank": int(local_rank), "device": int(dev.index),
+            "pci": f"{int(p.pci_domain_id):04x}:{int(p.pci_bus_id):02x}:{int(p.pci_device_id):02x}",
+            "uuid": str(getattr(p, "uuid", ""))}
+
+
+def shared_devices(ranks):
+    """{pci address: [ranks]} for every physical device that more than one rank runs on."""
+    by = {}
+    for r in ranks:
+        by.setdefault(r["pci"], []).append(r["rank"])
+    return {k: v for k, v in by.items() if len(v) > 1}
+
+
+def check_rank_devices(ranks, backend):
+    """None, or why this launch is refused: under nccl (RCCL) every rank must own its own GPU — two
+    ranks on one device would make an N-GPU line that N GPUs did not produce.  The gloo rehearsal
+    (several ranks on one GPU, tile sums staged through host memory) may share devices."""
+    shared = shared_devices(ranks)
+    if backend == "nccl" and shared:
+        return "ranks share a GPU under nccl: " + ", ".join(f"{k} <- ranks {v}" for k, v in sorted(shared.items()))
+    return None
+
+
 def main():
     args = parse()
     rc = launch_check(args)
@@ -304,6 +337,19 @@ def main():
     else:
         torch.cuda.set_device(0)
     coll_dev = torch.device("cpu") if gloo else dev   # where collective operands live
+    # which GPU every rank renders on (config.ranks): gathered before any work, and a launch whose
+    # nccl ranks share a device is refused (exit 2) on every rank alike
+    ident = rank_identity(dev, rank, local)
+    ranks = [ident]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, ident)
+        why = check_rank_devices(ranks, args.backend)
+        if why:
+            if rank == 0:
+                print(f"bench.py: {why}", file=sys.stderr)
+            dist.destroy_process_group()
+            sys.exit(2)
 
     from pyrenderer_amd import _native as N
     from pyrenderer_amd.device_scene import DeviceScene
@@ -405,23 +451,56 @@ def main():
     # trace launches per step at C5); the roofline is per launch
     launches_per_step = max(launches, 1) / args.steps
     t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=coll_dev)
+    # every rank's own timed-region wall time (imbalance shows as max / min)
+    per_rank = [t[0:1].clone() for _ in range(world)]
     if world > 1:
+        dist.all_gather(per_rank, t[0:1].clone())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_avg_ms = t.tolist()
+    rank_ms = [float(x.item()) * 1e3 / args.steps for x in per_rank]
+
+    # what batching buys: the same step with ONE frame per persistent launch, timed the
+    # same way (barrier + synchronize on both sides, max over ranks), after the main leg
+    single = None
+    if F > 1 and args.single_frame_steps > 0:
+        steps(1, 0)                                  # warm the single-frame buffers and launch shape
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ds.kernel_timing()
+        t1 = time.perf_counter()
+        for _ in range(args.single_frame_steps):
+            steps(1, N.PRT_FLAG_TIME)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el1 = time.perf_counter() - t1
+        k1_ms, k1_n = ds.kernel_timing()
+        t1v = torch.tensor([el1, k1_ms / max(k1_n, 1)], dtype=torch.float64, device=coll_dev)
+        if world > 1:
+            dist.all_reduce(t1v, op=dist.ReduceOp.MAX)
+        el1, k1_avg = t1v.tolist()
+        ms1 = el1 * 1e3 / args.single_frame_steps
+        single = {"frames_per_launch": 1, "steps": args.single_frame_steps, "ms_per_step": round(ms1, 4),
+                  "value": round(W * H * args.spp / (ms1 * 1e-3) / 1e6, 3),
+                  "kernel_avg_ms": round(k1_avg, 4), "launches_per_step": round(k1_n / args.single_frame_steps, 3),
+                  "note": "one frame per persistent launch (a one-shot render() of this frame); `value` above "
+                          "batches frames_per_launch frames per launch, each still rendered, reduced, gathered "
+                          "and scattered whole"}
 
     if rank == 0:
         samples_per_step = W * H * args.spp
         ms_per_step = elapsed * 1e3 / args.steps
         value = samples_per_step / (elapsed / args.steps) / 1e6
         # roofline of the dominant kernel (trace_kernel) on rank 0 (per launch)
-        per_rank = 1.0 / world
+        share = 1.0 / world
         n_px_rank = len(my_tiles) * T * T
         # the variant of this workload's launches (small launches take the phase-aligned kernel)
         kinfo = ds.kernel_info(n_items=int(round(n_px_rank * args.spp / launches_per_step)))
         if args.variant:
             kinfo = dict(kinfo, variant=args.variant)
         # SURVEY.md §8(d) algorithmic bytes per launch (module constants S8_*)
-        work_launch = per_rank / launches_per_step
+        work_launch = share / launches_per_step
         bytes_launch = ((S8_NODE * nodes + S8_TRI * tris + S8_LIGHT * shadow) * work_launch
                         + S8_PIXEL * n_px_rank / launches_per_step)
         kern_s = kern_avg_ms * 1e-3
@@ -520,7 +599,12 @@ def main():
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
                        "backend": (args.backend if world > 1 else None),
                        "tile_scheme": args.scheme, "frames_in_flight": n_streams, "frames_per_launch": -(-args.steps // -(-args.steps // F)),
-                       "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3)},
+                       "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3),
+                       "ranks": ranks},
+            # each rank's own wall time per step over the timed steps (value uses the max)
+            "rank_ms_per_step": {"min": round(min(rank_ms), 4), "max": round(max(rank_ms), 4),
+                                 "per_rank": [round(x, 4) for x in rank_ms]},
+            "single_frame": single,
             "roofline": roofline,
             "work_per_sample": {"nodes": round(nodes / samples_per_step, 2), "tris": round(tris / samples_per_step, 2),
                                 "ext_queries": round(ext / samples_per_step, 3),

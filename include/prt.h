@@ -38,7 +38,7 @@ extern "C" {
  * ABI 3 (this build): prt_render_frames_device (round 4) takes an output pitch between frames
  * (out_pitch, floats; 0 = packed), so a rank whose shard is shorter than its gather slot can render
  * straight into a padded per-frame buffer; PRT_FLAG_NO_PRIMARY_KERNEL, accepted by ABI 2, is
- * rejected with PRT_ERR_UNSUP; prt_scatter_frames added; variant ids 9 / 10 (the pooled kernel's
+ * rejected with PRT_ERR_UNSUP; prt_scatter_frames and prt_camera_rays added; variant ids 9 / 10 (the pooled kernel's
  * fused schedule, 7 / 6 waves per SIMD: extension traversals also answer the pooled shadow rays)
  * added, ids above 10 rejected with PRT_ERR_ARG. */
 #define PRT_ABI_VERSION 3
@@ -261,6 +261,15 @@ int prt_hit_all(void* scene, const float* rays, int64_t n, uint64_t seed, uint32
  * the render calls.  Runs the persistent trace kernel of prt_render_tiles.  Synchronous. */
 int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_t seed, uint32_t flags,
                    float* out_rgb);
+/* ABI 3: the primary rays of a render, as camera_kernel generates them for the trace kernels
+ * (main_taichi.py:89-95: u = (x + ti.random()) / (W - 1), v likewise, then CameraTaichi.gen_ray
+ * core/camera_taichi.py:47-74, the jitter and any lens draws from the stream keyed (seed, pixel,
+ * sample)): samples first_sample .. first_sample + spp - 1 of the tile set's pixels, item order
+ * [sample][slot] (slot order of prt_render_tiles).  out8 = n x 8 f32: origin.xyz, the RNG state
+ * after the camera's draws (u32 bits), direction.xyz, 0.  Parity / inspection entry point (the host
+ * gen_ray of PackedCamera is checked against it).  Synchronous. */
+int prt_camera_rays(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
+                    int n_tiles, int first_sample, int spp, uint64_t seed, float* out8);
 /* trace-kernel variant chosen for this scene's large launches when flags select none:
  * out4 = {variant, BVH arity (2 or 4), bit 0 scene LDS-resident | bit 1 quantised nodes,
  *         LDS traversal stack entries per lane: the instantiation set, or for the pooled kernel

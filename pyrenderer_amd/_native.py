@@ -74,6 +74,7 @@ EXPORTS = {
     "prt_comm_release": (None, []),
     "prt_scatter_tiles": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "prt_scatter_frames": (_i, [_vp, _vp, _vp, _i, _i, _i64, _i, _i, _i, _i, _i, _i64, _vp, _vp]),
+    "prt_camera_rays": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _vp]),
     "prt_render_tiles_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _u32, _vp, _vp]),
     "prt_render_frames_device": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _u64, _i, _i, _u32, _vp, _i64, _vp]),
     "prt_render_tiles_accumulate": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _u64, _u32, _vp]),

@@ -47,6 +47,39 @@ class PackedCamera:
         out[16:20] = self.sensor_dim
         return out
 
+    def gen_ray(self, u, v, lens=None):
+        """CameraTaichi.gen_ray (core/camera_taichi.py:47-74), which the reference's render loop calls
+        per sample (main_taichi.py:95): the ray through sensor coordinates (u, v) in [0, 1]^2, as
+        (origin, direction) float32 arrays of shape (..., 3) for scalar or array u, v.
+
+        f32 arithmetic in the reference's expression order — bit-identical to the kernel's gen_ray
+        (camera_kernel) and the oracle's.  With an aperture the origin is jittered by two uniform
+        draws per ray, as the reference's two rand() calls (the focus-distance scale kept):
+        `lens` (..., 2) supplies them (the kernel draws them from the sample's stream after the pixel
+        jitter); without it they come from numpy's default generator."""
+        f = np.float32
+        u = np.asarray(u, f)
+        v = np.asarray(v, f)
+        u, v = np.broadcast_arrays(u, v)
+        sd = self.sensor_dim
+        half = f(0.5)
+        rd = [(u - half) * sd[0] / half, (v - half) * sd[1] / half, np.full(u.shape, -sd[2], f), np.ones(u.shape, f)]
+        ro = [np.zeros(u.shape, f), np.zeros(u.shape, f), np.zeros(u.shape, f), np.ones(u.shape, f)]
+        if sd[3] > 0:
+            if lens is None:
+                lens = np.random.default_rng().random(u.shape + (2,), dtype=f)
+            lens = np.asarray(lens, f)
+            ro[0] = sd[2] * lens[..., 0] - sd[2] / f(2.0)
+            ro[1] = sd[2] * lens[..., 1] - sd[2] / f(2.0)
+        c = self.iview_cols          # row i = iview_c{i+1}
+        dw = [((rd[0] * c[i, 0] + rd[1] * c[i, 1]) + rd[2] * c[i, 2]) + rd[3] * c[i, 3] for i in range(4)]
+        ow = [((ro[0] * c[i, 0] + ro[1] * c[i, 1]) + ro[2] * c[i, 2]) + ro[3] * c[i, 3] for i in range(4)]
+        fr = [dw[i] - ow[i] for i in range(4)]
+        ln = np.sqrt(((fr[0] * fr[0] + fr[1] * fr[1]) + fr[2] * fr[2]) + fr[3] * fr[3])
+        origin = np.stack(ow[:3], axis=-1).astype(f)
+        direction = np.stack([fr[0] / ln, fr[1] / ln, fr[2] / ln], axis=-1).astype(f)
+        return origin, direction
+
 
 class Camera:
     def __init__(self, position, looking_at, up, resolution, fov=90, aperture=0, focal_dist=1.0):

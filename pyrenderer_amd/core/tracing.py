@@ -105,6 +105,18 @@ def render(scene, camera, *, spp, depth, seed=0, resolution=None, devices=(0,), 
     return tracer.render(camera.convert_to_taichi_camera().packed(), spp, seed, devices, tile, nee)
 
 
+def render_sums(scene, camera, *, spp, depth, seed=0, resolution=None, devices=(0,), tile=64, world=None,
+                nee="reference"):
+    """Per-pixel radiance SUMS (W, H, 3) float32 [x][y] over spp samples — the reference's `pixels`
+    field after spp render() passes (main_taichi.py:97); render() returns these / spp."""
+    W, H = resolution if resolution is not None else camera.resolution
+    world = world or build_world(scene, devices)
+    tracer = PathTracer(world, depth, int(W), int(H))
+    if spp <= 0:
+        return np.zeros((int(W), int(H), 3), np.float32)
+    return tracer.render_sums(camera.convert_to_taichi_camera().packed(), spp, seed, devices, tile, nee_flags(nee))
+
+
 class Accumulator:
     """Progressive rendering on one device (main_taichi.py:108-127).
 

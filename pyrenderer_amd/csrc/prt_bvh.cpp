@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -47,114 +48,6 @@ struct TNode {
 };
 
 constexpr int kMaxBins = 64;
-
-struct Builder {
-    const float* tv;
-    int64_t n;
-    int max_leaf;
-    int bins = 32;             // SAH bins per axis (env PRT_SAH_BINS, 2..64)
-    double ct = 0.5;           // SAH cost of a node step relative to one triangle test (env PRT_SAH_CT)
-    int leaf_min = 2;          // ranges of <= leaf_min triangles always become leaves (env PRT_LEAF_MIN)
-    std::vector<Box> tb;
-    std::vector<float> cen;    // n*3
-    std::vector<int32_t> idx;  // permutation
-    std::vector<TNode> nodes;
-    int32_t max_depth = 0;
-    int64_t leaves = 0;
-
-    int32_t build(int64_t first, int64_t count, int depth) {
-        int32_t me = (int32_t)nodes.size();
-        nodes.emplace_back();
-        Box b, cb;
-        for (int64_t i = first; i < first + count; ++i) {
-            b.grow(tb[idx[i]]);
-            cb.grow(&cen[3 * (size_t)idx[i]]);
-        }
-        nodes[me].box = b;
-        max_depth = std::max(max_depth, depth);
-        if (count <= max_leaf && (count <= leaf_min || depth > 32)) return make_leaf(me, first, count);
-        if (depth >= 32) {
-            // depth guard (bounds the traversal stack): object median on the widest centroid axis
-            int ax = 0;
-            for (int k = 1; k < 3; ++k)
-                if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
-            int64_t mid = first + count / 2;
-            std::nth_element(idx.begin() + first, idx.begin() + mid, idx.begin() + first + count,
-                             [&](int32_t a, int32_t c) { return cen[3 * (size_t)a + ax] < cen[3 * (size_t)c + ax]; });
-            int32_t l = build(first, mid - first, depth + 1);
-            int32_t r = build(mid, first + count - mid, depth + 1);
-            nodes[me].left = l;
-            nodes[me].right = r;
-            return me;
-        }
-        // binned SAH over the three axes
-        double best_cost = DBL_MAX;
-        int best_axis = -1, best_split = -1;
-        for (int ax = 0; ax < 3; ++ax) {
-            float ext = cb.hi[ax] - cb.lo[ax];
-            if (!(ext > 0.0f)) continue;
-            const int kBins = bins;
-            Box bins[kMaxBins];
-            int64_t cnt[kMaxBins] = {0};
-            double scale = kBins / (double)ext;
-            for (int64_t i = first; i < first + count; ++i) {
-                int k = (int)(((double)cen[3 * (size_t)idx[i] + ax] - cb.lo[ax]) * scale);
-                k = std::min(std::max(k, 0), kBins - 1);
-                cnt[k]++;
-                bins[k].grow(tb[idx[i]]);
-            }
-            double ra[kMaxBins];
-            int64_t rc[kMaxBins];
-            Box acc;
-            int64_t c = 0;
-            for (int k = kBins - 1; k > 0; --k) {
-                acc.grow(bins[k]); c += cnt[k];
-                ra[k] = acc.area(); rc[k] = c;
-            }
-            Box lacc;
-            int64_t lc = 0;
-            for (int k = 0; k < kBins - 1; ++k) {
-                lacc.grow(bins[k]); lc += cnt[k];
-                if (lc == 0 || rc[k + 1] == 0) continue;
-                double cost = lacc.area() * (double)lc + ra[k + 1] * (double)rc[k + 1];
-                if (cost < best_cost) { best_cost = cost; best_axis = ax; best_split = k; }
-            }
-        }
-        double parent_area = b.area();
-        double leaf_cost = (double)count;
-        double split_cost = parent_area > 0.0 ? ct + best_cost / parent_area : DBL_MAX;
-        if (count <= max_leaf && !(split_cost < leaf_cost)) return make_leaf(me, first, count);
-        int64_t mid;
-        if (best_axis < 0) {
-            mid = first + count / 2;  // all centroids coincide: split the range
-        } else {
-            float ext = cb.hi[best_axis] - cb.lo[best_axis];
-            const int kBins = bins;
-            double scale = kBins / (double)ext;
-            auto it = std::partition(idx.begin() + first, idx.begin() + first + count, [&](int32_t t) {
-                int k = (int)(((double)cen[3 * (size_t)t + best_axis] - cb.lo[best_axis]) * scale);
-                k = std::min(std::max(k, 0), kBins - 1);
-                return k <= best_split;
-            });
-            mid = it - idx.begin();
-            if (mid == first || mid == first + count) mid = first + count / 2;
-        }
-        int32_t l = build(first, mid - first, depth + 1);
-        int32_t r = build(mid, first + count - mid, depth + 1);
-        nodes[me].left = l;
-        nodes[me].right = r;
-        return me;
-    }
-
-    int32_t make_leaf(int32_t me, int64_t first, int64_t count) {
-        nodes[me].first = first;
-        nodes[me].count = (int32_t)count;
-        leaves++;
-        return me;
-    }
-};
-
-inline float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
 
 // ---------------------------------------------------------- early split clipping
 // A triangle far larger than the scene's typical one (the Cornell walls among config 4's
@@ -246,14 +139,297 @@ inline Box outward_f32(const RefBox& r, const Box& tri_box) {
     return b;
 }
 
+
+// Binned-SAH builder over references (a triangle, or an early-split-clipping piece of one), with
+// spatial splits (Stich, Friedrich & Dietrich 2009, "Spatial Splits in Bounding Volume
+// Hierarchies"; env PRT_SBVH=0 turns them off): where the best object split's two children overlap
+// (their intersection's area > alpha x the root's, env PRT_SBVH_ALPHA, default 1e-5), the node's
+// box is also cut by 32 planes per axis, every reference chopped into the bins it spans (its triangle
+// clipped to the reference box and the bin, bounds in double rounded outward to f32), and the
+// cheaper of the two splits is taken.  A reference straddling a spatial split plane goes to both
+// sides as two references, each bounding the triangle's part on its side — unless moving it whole
+// to one side costs less (reference unsplitting).  Duplicates stop at a budget of references
+// (env PRT_SBVH_BUDGET x the initial count, default 1.3).  Every reference's record is its whole
+// triangle, so a leaf tests the same Moller-Trumbore on it and the closest (t, id) is unchanged;
+// the union of a triangle's reference boxes covers it.
+struct Builder {
+    const float* tv;           // triangle vertices (n_tri x 9)
+    int max_leaf;
+    int bins = 32;             // SAH bins per axis (env PRT_SAH_BINS, 2..64)
+    double ct = 0.5;           // SAH cost of a node step relative to one triangle test (env PRT_SAH_CT)
+    int leaf_min = 2;          // ranges of <= leaf_min triangles always become leaves (env PRT_LEAF_MIN)
+    bool sbvh = false;         // spatial splits (env PRT_SBVH=1; off by default)
+    double alpha = 1e-5;       // overlap threshold relative to the root's area (env PRT_SBVH_ALPHA)
+    double min_overlap = 0.0;  // alpha x root area
+    int64_t ref_budget = 0;    // spatial splits stop once the references reach this count
+    std::vector<Box> tb;       // per reference: box
+    std::vector<float> cen;    // per reference: box centre (3)
+    std::vector<int32_t> ref_tri;   // per reference: original triangle
+    std::vector<int32_t> order;     // leaf order of the references (output)
+    std::vector<TNode> nodes;
+    int32_t max_depth = 0;
+    int64_t leaves = 0, spatial_splits = 0;
+
+    void set_centre(int32_t r) {
+        for (int k = 0; k < 3; ++k) cen[3 * (size_t)r + k] = 0.5f * (tb[(size_t)r].lo[k] + tb[(size_t)r].hi[k]);
+    }
+    // the part of reference r's triangle inside box `cell` (intersected with the reference's box),
+    // rounded outward; false when empty
+    bool clip_ref(int32_t r, double lo_ax, double hi_ax, int ax, Box* out) const {
+        const float* t = tv + 9 * (size_t)ref_tri[(size_t)r];
+        double v[3][3];
+        for (int a = 0; a < 3; ++a)
+            for (int k = 0; k < 3; ++k) v[a][k] = (double)t[3 * a + k];
+        const Box& rb = tb[(size_t)r];
+        RefBox cell;
+        for (int k = 0; k < 3; ++k) { cell.lo[k] = rb.lo[k]; cell.hi[k] = rb.hi[k]; }
+        cell.lo[ax] = std::max(cell.lo[ax], lo_ax);
+        cell.hi[ax] = std::min(cell.hi[ax], hi_ax);
+        if (!(cell.lo[ax] <= cell.hi[ax])) return false;
+        RefBox cb;
+        if (!clip_bounds(v, cell, &cb)) return false;
+        Box tri_box;
+        tri_box.grow(t); tri_box.grow(t + 3); tri_box.grow(t + 6);
+        *out = outward_f32(cb, tri_box);
+        // never beyond the reference's own box (the parent region)
+        for (int k = 0; k < 3; ++k) {
+            out->lo[k] = std::max(out->lo[k], rb.lo[k]);
+            out->hi[k] = std::min(out->hi[k], rb.hi[k]);
+        }
+        return out->lo[0] <= out->hi[0] && out->lo[1] <= out->hi[1] && out->lo[2] <= out->hi[2];
+    }
+
+    static Box meet(const Box& a, const Box& b) {
+        Box m;
+        for (int k = 0; k < 3; ++k) { m.lo[k] = std::max(a.lo[k], b.lo[k]); m.hi[k] = std::min(a.hi[k], b.hi[k]); }
+        for (int k = 0; k < 3; ++k)
+            if (!(m.lo[k] <= m.hi[k])) return Box();
+        return m;
+    }
+
+    int32_t make_leaf(int32_t me, const std::vector<int32_t>& refs) {
+        nodes[me].first = (int64_t)order.size();
+        nodes[me].count = (int32_t)refs.size();
+        order.insert(order.end(), refs.begin(), refs.end());
+        leaves++;
+        return me;
+    }
+
+    int32_t build(std::vector<int32_t>& refs, int depth) {
+        const int64_t count = (int64_t)refs.size();
+        int32_t me = (int32_t)nodes.size();
+        nodes.emplace_back();
+        Box b, cb;
+        for (int32_t r : refs) {
+            b.grow(tb[(size_t)r]);
+            cb.grow(&cen[3 * (size_t)r]);
+        }
+        nodes[me].box = b;
+        max_depth = std::max(max_depth, depth);
+        if (count <= max_leaf && (count <= leaf_min || depth > 32)) return make_leaf(me, refs);
+        std::vector<int32_t> left, right;
+        if (depth >= 32) {
+            // depth guard (bounds the traversal stack): object median on the widest centroid axis
+            int ax = 0;
+            for (int k = 1; k < 3; ++k)
+                if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
+            const int64_t mid = count / 2;
+            std::nth_element(refs.begin(), refs.begin() + mid, refs.end(),
+                             [&](int32_t a, int32_t c) { return cen[3 * (size_t)a + ax] < cen[3 * (size_t)c + ax]; });
+            left.assign(refs.begin(), refs.begin() + mid);
+            right.assign(refs.begin() + mid, refs.end());
+            std::vector<int32_t>().swap(refs);
+            nodes[me].left = build(left, depth + 1);
+            nodes[me].right = build(right, depth + 1);
+            return me;
+        }
+        // binned SAH object split over the three axes
+        double best_cost = DBL_MAX;
+        int best_axis = -1, best_split = -1;
+        Box best_l, best_r;
+        for (int ax = 0; ax < 3; ++ax) {
+            float ext = cb.hi[ax] - cb.lo[ax];
+            if (!(ext > 0.0f)) continue;
+            const int kBins = bins;
+            Box bb[kMaxBins];
+            int64_t cnt[kMaxBins] = {0};
+            double scale = kBins / (double)ext;
+            for (int32_t r : refs) {
+                int k = (int)(((double)cen[3 * (size_t)r + ax] - cb.lo[ax]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                cnt[k]++;
+                bb[k].grow(tb[(size_t)r]);
+            }
+            Box rbx[kMaxBins];
+            int64_t rc[kMaxBins];
+            Box acc;
+            int64_t c = 0;
+            for (int k = kBins - 1; k > 0; --k) {
+                acc.grow(bb[k]); c += cnt[k];
+                rbx[k] = acc; rc[k] = c;
+            }
+            Box lacc;
+            int64_t lc = 0;
+            for (int k = 0; k < kBins - 1; ++k) {
+                lacc.grow(bb[k]); lc += cnt[k];
+                if (lc == 0 || rc[k + 1] == 0) continue;
+                double cost = lacc.area() * (double)lc + rbx[k + 1].area() * (double)rc[k + 1];
+                if (cost < best_cost) {
+                    best_cost = cost; best_axis = ax; best_split = k;
+                    best_l = lacc; best_r = rbx[k + 1];
+                }
+            }
+        }
+        // spatial split: only where the object split's children overlap, within the reference budget
+        double s_cost = DBL_MAX;
+        int s_axis = -1, s_split = -1;
+        if (sbvh && best_axis >= 0 && (int64_t)tb.size() < ref_budget && meet(best_l, best_r).area() > min_overlap) {
+            for (int ax = 0; ax < 3; ++ax) {
+                const double lo = b.lo[ax], ext = (double)b.hi[ax] - b.lo[ax];
+                if (!(ext > 0.0)) continue;
+                const int kBins = bins;
+                const double w = ext / kBins;
+                Box bb[kMaxBins];
+                int64_t entry[kMaxBins] = {0}, exit_[kMaxBins] = {0};
+                for (int32_t r : refs) {
+                    const Box& rb = tb[(size_t)r];
+                    int b0 = (int)(((double)rb.lo[ax] - lo) / w), b1 = (int)(((double)rb.hi[ax] - lo) / w);
+                    b0 = std::min(std::max(b0, 0), kBins - 1);
+                    b1 = std::min(std::max(b1, b0), kBins - 1);
+                    entry[b0]++;
+                    exit_[b1]++;
+                    if (b0 == b1) {
+                        bb[b0].grow(rb);
+                        continue;
+                    }
+                    for (int k = b0; k <= b1; ++k) {
+                        Box part;
+                        const double pl = k == b0 ? -INFINITY : lo + w * k, ph = k == b1 ? INFINITY : lo + w * (k + 1);
+                        if (clip_ref(r, pl, ph, ax, &part)) bb[k].grow(part);
+                    }
+                }
+                Box rbx[kMaxBins];
+                int64_t rc[kMaxBins];
+                Box acc;
+                int64_t c = 0;
+                for (int k = kBins - 1; k > 0; --k) {
+                    acc.grow(bb[k]); c += exit_[k];
+                    rbx[k] = acc; rc[k] = c;
+                }
+                Box lacc;
+                int64_t lc = 0;
+                for (int k = 0; k < kBins - 1; ++k) {
+                    lacc.grow(bb[k]); lc += entry[k];
+                    if (lc == 0 || rc[k + 1] == 0) continue;
+                    double cost = lacc.area() * (double)lc + rbx[k + 1].area() * (double)rc[k + 1];
+                    if (cost < s_cost) { s_cost = cost; s_axis = ax; s_split = k; }
+                }
+            }
+        }
+        const bool spatial = s_axis >= 0 && s_cost < best_cost;
+        const double split_sah = spatial ? s_cost : best_cost;
+        double parent_area = b.area();
+        double leaf_cost = (double)count;
+        double split_cost = parent_area > 0.0 ? ct + split_sah / parent_area : DBL_MAX;
+        if (count <= max_leaf && !(split_cost < leaf_cost)) return make_leaf(me, refs);
+        if (spatial) {
+            spatial_splits++;
+            const int ax = s_axis;
+            const double lo = b.lo[ax], w = ((double)b.hi[ax] - b.lo[ax]) / bins;
+            const double plane = lo + w * (s_split + 1);
+            // classify by the same bins as the search; straddling references are split or moved whole
+            std::vector<int32_t> straddle;
+            Box lb, rb_;
+            for (int32_t r : refs) {
+                const Box& x = tb[(size_t)r];
+                int b0 = (int)(((double)x.lo[ax] - lo) / w), b1 = (int)(((double)x.hi[ax] - lo) / w);
+                b0 = std::min(std::max(b0, 0), bins - 1);
+                b1 = std::min(std::max(b1, b0), bins - 1);
+                if (b1 <= s_split) { left.push_back(r); lb.grow(x); }
+                else if (b0 > s_split) { right.push_back(r); rb_.grow(x); }
+                else straddle.push_back(r);
+            }
+            std::vector<int32_t>().swap(refs);
+            for (int32_t r : straddle) {
+                Box pl, pr;
+                const bool hl = clip_ref(r, -INFINITY, plane, ax, &pl), hr = clip_ref(r, plane, INFINITY, ax, &pr);
+                if (!hr || (!hl && !hr)) { left.push_back(r); lb.grow(tb[(size_t)r]); continue; }
+                if (!hl) { right.push_back(r); rb_.grow(tb[(size_t)r]); continue; }
+                // reference unsplitting (Stich et al. 2009 §4.3): whole to one side when cheaper
+                const double nl = (double)left.size() + 1, nr = (double)right.size() + 1;
+                Box lsplit = lb, rsplit = rb_, lwhole = lb, rwhole = rb_;
+                lsplit.grow(pl); rsplit.grow(pr);
+                lwhole.grow(tb[(size_t)r]); rwhole.grow(tb[(size_t)r]);
+                const double c_split = lsplit.area() * nl + rsplit.area() * nr;
+                const double c_left = lwhole.area() * nl + rb_.area() * (nr - 1);
+                const double c_right = lb.area() * (nl - 1) + rwhole.area() * nr;
+                if ((int64_t)tb.size() >= ref_budget || (c_left <= c_split && c_left <= c_right)) {
+                    left.push_back(r); lb = lwhole;
+                } else if (c_right <= c_split) {
+                    right.push_back(r); rb_ = rwhole;
+                } else {
+                    const int32_t r2 = (int32_t)tb.size();
+                    tb[(size_t)r] = pl;
+                    set_centre(r);
+                    tb.push_back(pr);
+                    ref_tri.push_back(ref_tri[(size_t)r]);
+                    cen.resize(cen.size() + 3);
+                    set_centre(r2);
+                    left.push_back(r); lb = lsplit;
+                    right.push_back(r2); rb_ = rsplit;
+                }
+            }
+            if (left.empty() || right.empty()) {
+                // degenerate plane (everything on one side): object median instead
+                std::vector<int32_t> all(left);
+                all.insert(all.end(), right.begin(), right.end());
+                left.clear(); right.clear();
+                const int64_t mid = (int64_t)all.size() / 2;
+                left.assign(all.begin(), all.begin() + mid);
+                right.assign(all.begin() + mid, all.end());
+            }
+        } else if (best_axis < 0) {
+            const int64_t mid = count / 2;  // all centroids coincide: split the range
+            left.assign(refs.begin(), refs.begin() + mid);
+            right.assign(refs.begin() + mid, refs.end());
+            std::vector<int32_t>().swap(refs);
+        } else {
+            float ext = cb.hi[best_axis] - cb.lo[best_axis];
+            const int kBins = bins;
+            double scale = kBins / (double)ext;
+            auto it = std::partition(refs.begin(), refs.end(), [&](int32_t t) {
+                int k = (int)(((double)cen[3 * (size_t)t + best_axis] - cb.lo[best_axis]) * scale);
+                k = std::min(std::max(k, 0), kBins - 1);
+                return k <= best_split;
+            });
+            int64_t mid = it - refs.begin();
+            if (mid == 0 || mid == count) mid = count / 2;
+            left.assign(refs.begin(), refs.begin() + mid);
+            right.assign(refs.begin() + mid, refs.end());
+            std::vector<int32_t>().swap(refs);
+        }
+        int32_t l = build(left, depth + 1);
+        int32_t r = build(right, depth + 1);
+        nodes[me].left = l;
+        nodes[me].right = r;
+        return me;
+    }
+};
+
+inline float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
+
 }  // namespace
 
 bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, std::string* err) {
     if (max_leaf < 1 || max_leaf > kMaxLeaf) { *err = "max_leaf must be in [1, 8]"; return false; }
     if (n_tri < 0 || n_tri >= ((int64_t)1 << 27)) { *err = "triangle count out of range (< 2^27)"; return false; }
     Builder B;
-    B.tv = tri_v; B.n = n_tri; B.max_leaf = max_leaf;
+    B.tv = tri_v; B.max_leaf = max_leaf;
     if (const char* e = std::getenv("PRT_SAH_BINS")) B.bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
+    if (const char* e = std::getenv("PRT_SBVH")) B.sbvh = std::atoi(e) != 0;
+    if (const char* e = std::getenv("PRT_SBVH_ALPHA")) B.alpha = std::max(0.0, std::atof(e));
+    double budget = 1.3;
+    if (const char* e = std::getenv("PRT_SBVH_BUDGET")) budget = std::max(1.0, std::atof(e));
     if (const char* e = std::getenv("PRT_SAH_CT")) B.ct = std::max(0.0, std::atof(e));
     if (const char* e = std::getenv("PRT_LEAF_MIN")) B.leaf_min = std::max(1, std::min(max_leaf, std::atoi(e)));
     std::vector<Box> tri_box((size_t)n_tri);
@@ -277,7 +453,7 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     // area exceeds esc_beta x the mean (env PRT_ESC_BETA, 0 = off; at most 2 n_tri + 4096)
     double esc_beta = 64.0;
     if (const char* e = std::getenv("PRT_ESC_BETA")) esc_beta = std::max(0.0, std::atof(e));
-    std::vector<int32_t> ref_tri;
+    std::vector<int32_t>& ref_tri = B.ref_tri;
     ref_tri.reserve((size_t)n_tri);
     // the cap stays below the 2^27 references the leaf encoding addresses: past it every further
     // triangle keeps one reference (a scene with < 2^27 triangles always builds)
@@ -308,26 +484,30 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
             }
         }
     }
-    const int64_t n_ref = (int64_t)B.tb.size();
-    if (n_ref >= ((int64_t)1 << 27)) { *err = "too many BVH references (< 2^27)"; return false; }
-    B.n = n_ref;
-    B.cen.resize((size_t)n_ref * 3);
-    B.idx.resize((size_t)n_ref);
-    for (int64_t i = 0; i < n_ref; ++i) {
-        const Box& b = B.tb[(size_t)i];
-        for (int k = 0; k < 3; ++k) B.cen[3 * (size_t)i + k] = 0.5f * (b.lo[k] + b.hi[k]);
-        B.idx[(size_t)i] = (int32_t)i;
+    const int64_t n_ref0 = (int64_t)B.tb.size();
+    if (n_ref0 >= ((int64_t)1 << 27)) { *err = "too many BVH references (< 2^27)"; return false; }
+    B.cen.resize((size_t)n_ref0 * 3);
+    std::vector<int32_t> all((size_t)n_ref0);
+    for (int64_t i = 0; i < n_ref0; ++i) {
+        B.set_centre((int32_t)i);
+        all[(size_t)i] = (int32_t)i;
     }
+    // spatial splits add references up to the budget, below the 2^27 the leaf encoding addresses
+    B.ref_budget = std::min<int64_t>((int64_t)((double)n_ref0 * budget), ((int64_t)1 << 27) - 1);
     float extent = scene.valid() ? std::max({scene.hi[0] - scene.lo[0], scene.hi[1] - scene.lo[1], scene.hi[2] - scene.lo[2]}) : 0.0f;
     // Padding: ~8 ulps of the largest coordinate magnitude / extent.  Keeps the
     // slab test conservative against Moller-Trumbore accepting hit points that
     // lie a rounding error outside the triangle (axis-aligned Cornell edges).
     float pad = std::max(max_abs, extent) * 1e-6f + 1e-30f;
     int32_t root = -1;
-    if (n_ref > 0) {
-        B.nodes.reserve((size_t)(2 * n_ref / std::max(1, max_leaf / 2) + 8));
-        root = B.build(0, n_ref, 0);
+    if (n_ref0 > 0) {
+        B.nodes.reserve((size_t)(2 * n_ref0 / std::max(1, max_leaf / 2) + 8));
+        if (scene.valid()) B.min_overlap = B.alpha * scene.area();
+        root = B.build(all, 0);
     }
+    // every reference sits in exactly one leaf: the leaf order is the triangle records' order
+    const int64_t n_ref = (int64_t)B.order.size();
+    if (n_ref != (int64_t)B.tb.size()) { *err = "internal: BVH references lost in the build"; return false; }
     // flatten: inner nodes in DFS preorder; leaves become child references
     std::vector<int32_t> inner_id(B.nodes.size(), -1);
     std::vector<int32_t> stack;
@@ -384,7 +564,7 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
         out->n_nodes = n_inner;
     }
     out->order.resize((size_t)n_ref);
-    for (int64_t s = 0; s < n_ref; ++s) out->order[(size_t)s] = ref_tri[(size_t)B.idx[(size_t)s]];
+    for (int64_t s = 0; s < n_ref; ++s) out->order[(size_t)s] = ref_tri[(size_t)B.order[(size_t)s]];
     out->tris.assign((size_t)n_ref * 12, 0.0f);
     for (int64_t s = 0; s < n_ref; ++s) {
         int32_t o = out->order[(size_t)s];
@@ -407,6 +587,11 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
         for (const TNode& nd : B.nodes) sah += nd.box.area() / ra * (nd.count > 0 ? (double)nd.count : 1.0);
     }
     out->sah_cost = sah;
+    out->n_spatial = B.spatial_splits;
+    if (std::getenv("PRT_BVH_VERBOSE"))
+        std::fprintf(stderr, "prt_bvh: %lld triangles, %lld references (%lld before spatial splits), %lld spatial "
+                             "splits, %lld leaves, depth %d, SAH %.3f\n", (long long)n_tri, (long long)n_ref,
+                     (long long)n_ref0, (long long)B.spatial_splits, (long long)B.leaves, (int)out->depth, sah);
     return true;
 }
 

@@ -72,9 +72,16 @@ void frame_rows(F3 n, float* out12) {
 // log, 160..175 the pooled kernel's lane table (STATS builds)
 constexpr int kStatWords = 192;
 
+// Device buffer owned by its holder: freed by release() or, at the latest, by the destructor (the
+// per-call buffers of prt_trace_rays / prt_closest_hits / prt_hit_all are locals, freed on return
+// after their stream has been synchronised; round 4 leaked them on every call).  Not copyable.
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
     hipError_t ensure(size_t want) {
         if (want <= bytes) return hipSuccess;
         if (p) (void)hipFree(p);
@@ -380,6 +387,23 @@ int trace_setup(Scene* s, RenderCtx* cx, uint32_t flags, int64_t n_items, prt::T
     return PRT_OK;
 }
 
+// Camera and frame part of a launch's parameters (camera_kernel's gen_ray inputs): the record, the
+// pinhole shortcut's host-evaluated constant terms (TraceParams::cam_fast), resolution and tiling.
+void camera_params(prt::TraceParams& P, const float* cam, int W, int H, int tw, int th) {
+    std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
+    P.cam_fast = camera_is_fast(cam) ? 1 : 0;
+    const float rd2 = -cam[18];
+    for (int i = 0; i < 3; ++i) {
+        const float* c = cam + 4 * i;
+        P.cam_o[i] = 0.0f * c[0] + 0.0f * c[1] + 0.0f * c[2] + 1.0f * c[3];
+        P.cam_k[i] = rd2 * c[2];
+    }
+    P.W = W; P.H = H;
+    P.wm1 = (float)(W - 1); P.hm1 = (float)(H - 1);
+    P.log_tw = __builtin_ctz((unsigned)tw);
+    P.log_tpx = __builtin_ctz((unsigned)(tw * th));
+}
+
 // Enqueue the whole render of a tile set on `stream`, result in d_acc: samples
 // first_sample .. first_sample + spp - 1 of every pixel; `accumulate` adds them onto the
 // sums already in d_acc (progressive rendering) instead of overwriting them.
@@ -456,22 +480,9 @@ int enqueue_render(Scene* s, RenderCtx* cx, const float* cam, int W, int H, int 
 
     prt::TraceParams P;
     scene_params(s, P);
-    std::memcpy(P.cam, cam, sizeof(float) * PRT_CAM_FLOATS);
-    {
-        P.cam_fast = cam_fast ? 1 : 0;
-        P.rays = (const float4*)cx->rays.p;
-        P.ray_o = cam_fast ? nullptr : (const float4*)cx->rays_o.p;
-        const float rd2 = -cam[18];
-        for (int i = 0; i < 3; ++i) {
-            const float* c = cam + 4 * i;
-            P.cam_o[i] = 0.0f * c[0] + 0.0f * c[1] + 0.0f * c[2] + 1.0f * c[3];
-            P.cam_k[i] = rd2 * c[2];
-        }
-    }
-    P.W = W; P.H = H;
-    P.wm1 = (float)(W - 1); P.hm1 = (float)(H - 1);
-    P.log_tw = __builtin_ctz((unsigned)tw);
-    P.log_tpx = __builtin_ctz((unsigned)(tw * th));
+    camera_params(P, cam, W, H, tw, th);
+    P.rays = (const float4*)cx->rays.p;
+    P.ray_o = cam_fast ? nullptr : (const float4*)cx->rays_o.p;
     P.tile_xy = (const uint32_t*)cx->tiles.p;
     P.n_slots = (int)n_slots;
     P.depth = depth;
@@ -941,6 +952,54 @@ int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_
     HIP_TRY(hipStreamSynchronize(s->stream));
     if (take_fault_at(cx->work) != 0)
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
+    return PRT_OK;
+}
+
+int prt_camera_rays(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
+                    int n_tiles, int first_sample, int spp, uint64_t seed, float* out8) {
+    auto* s = (Scene*)scene;
+    if (int rc = check_render_args(s, cam, W, H, tw, th, tile_ids, n_tiles, spp, 1)) return rc;
+    if (first_sample < 0 || (int64_t)first_sample + spp > INT32_MAX)
+        return fail(PRT_ERR_ARG, "sample indices must stay in [0, 2^31)");
+    const int64_t n_slots = (int64_t)n_tiles * tw * th, n = n_slots * spp;
+    if (n == 0) return PRT_OK;
+    if (!out8) return fail(PRT_ERR_ARG, "out8 is NULL");
+    if (n >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many rays in one call (< 2^31)");
+    DeviceGuard g(s->device);
+    const int tiles_x = (W + tw - 1) / tw;
+    std::vector<uint32_t> origins((size_t)n_tiles);
+    for (int i = 0; i < n_tiles; ++i)
+        origins[(size_t)i] = ((uint32_t)((tile_ids[i] % tiles_x) * tw) << 16) | (uint32_t)((tile_ids[i] / tiles_x) * th);
+    DevBuf d_tiles, d_rays, d_org;
+    HIP_TRY(d_tiles.ensure(sizeof(uint32_t) * (size_t)n_tiles));
+    HIP_TRY(d_rays.ensure(16 * (size_t)n));
+    HIP_TRY(d_org.ensure(16 * (size_t)n));
+    HIP_TRY(hipMemcpyAsync(d_tiles.p, origins.data(), sizeof(uint32_t) * (size_t)n_tiles, hipMemcpyHostToDevice,
+                           s->stream));
+    prt::TraceParams P;
+    scene_params(s, P);
+    camera_params(P, cam, W, H, tw, th);
+    P.tile_xy = (const uint32_t*)d_tiles.p;
+    P.n_slots = (int)n_slots;
+    P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
+    P.s0 = first_sample;
+    P.j0 = 0;
+    P.n_items = (uint64_t)n;
+    P.cam_clears = 0;
+    HIP_TRY(prt::launch_camera(P, (float4*)d_rays.p, P.cam_fast ? nullptr : (float4*)d_org.p, s->stream));
+    std::vector<float> r((size_t)n * 4), o(P.cam_fast ? 0 : (size_t)n * 4);
+    HIP_TRY(hipMemcpyAsync(r.data(), d_rays.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    if (!P.cam_fast) HIP_TRY(hipMemcpyAsync(o.data(), d_org.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    for (int64_t i = 0; i < n; ++i) {
+        float* q = out8 + 8 * i;
+        for (int k = 0; k < 3; ++k) {
+            q[k] = P.cam_fast ? P.cam_o[k] : o[(size_t)(4 * i + k)];
+            q[4 + k] = r[(size_t)(4 * i + k)];
+        }
+        q[3] = r[(size_t)(4 * i + 3)];   // the RNG state after the camera's draws (u32 bits)
+        q[7] = 0.0f;
+    }
     return PRT_OK;
 }
 

@@ -1727,7 +1727,10 @@ void trace_kernel_pool(TraceParams P) {
                         visit_node4<STATS, 1, LdsStack16, false, true>(g_nodes, cur, sp, stk, inv, oi, sx, 0, 0, kTMin,
                                                                        best, cn);
 #endif
-                        if (STATS) wave_tick(cn.wi, cn.li);
+                        if (STATS) {
+                            wave_tick(cn.wi, cn.li);
+                            cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
+                        }
                         if (cur < 0 && leaf >= 0) {
                             leaf = cur;
                             cur = stk.get(sp);

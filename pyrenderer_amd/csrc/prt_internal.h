@@ -35,6 +35,7 @@ struct BvhHost {
     int64_t n_leaves = 0;
     float pad = 0.0f;              // absolute box padding applied
     double sah_cost = 0.0;
+    int64_t n_spatial = 0;         // spatial splits taken (SBVH, prt_bvh.cpp)
 };
 
 // BVH4 collapsed from the BVH2 (same triangle order and leaf encoding).

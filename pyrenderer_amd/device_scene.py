@@ -181,6 +181,17 @@ class DeviceScene:
                                            H, int(n_frames), int(src_frame_pitch), ctypes.c_void_p(d_frames_ptr),
                                            ctypes.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def camera_rays(self, cam, W, H, tw, th, tile_ids, first_sample, spp, seed=0):
+        """prt_camera_rays: the primary rays camera_kernel hands the trace kernels, (origin (n, 3),
+        direction (n, 3), rng state (n,) u32) in [sample][slot] order."""
+        cam = np.ascontiguousarray(cam, np.float32)
+        tile_ids = np.ascontiguousarray(tile_ids, np.int32)
+        n = tile_ids.shape[0] * tw * th * spp
+        out = np.zeros((n, 8), np.float32)
+        N.check(N.lib().prt_camera_rays(self.h, N.ptr(cam), W, H, tw, th, N.ptr(tile_ids), tile_ids.shape[0],
+                                        int(first_sample), int(spp), int(seed), N.ptr(out)))
+        return out[:, 0:3].copy(), out[:, 4:7].copy(), out[:, 3].copy().view(np.uint32)
+
     def closest_hits(self, o, d, tmin, tmax, any_hit=False, quantized=False):
         """World.hit_all on the GPU for arrays of rays: (hit_id, t); id -1 = miss."""
         rays = pack_rays(o, d, tmin, tmax)

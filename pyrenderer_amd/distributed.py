@@ -64,13 +64,16 @@ class TileShard:
     def gather(self, group=None, n_frames=1):
         """Collective: rank 0 receives every rank's tile sums of frames 0 .. n_frames-1 in ONE
         gather (no-op for world 1).  Runs on torch's current stream: callers that rendered on
-        another stream enter it first, and a later scatter() on the same stream is ordered after
-        the receive (ProcessGroupNCCL makes the current stream wait for its collective stream
-        when the work is enqueued)."""
+        another stream enter it first (ProcessGroupNCCL's collective stream waits for the current
+        one when the gather is enqueued, so the send follows the render).  The receive side is
+        ordered explicitly: the gather is issued asynchronously and its work's wait() makes the
+        current stream wait for the collective stream (nccl; gloo: the host waits), so a
+        scatter_frames() enqueued next on this stream reads the received tiles."""
         if self.world > 1:
             if self.host_staging:
                 self.wire[:n_frames].copy_(self.bufs[:n_frames])   # synchronous device-to-host copy
-            dist.gather(self.wire[:n_frames], self.gather_list(n_frames), dst=0, group=group)
+            work = dist.gather(self.wire[:n_frames], self.gather_list(n_frames), dst=0, group=group, async_op=True)
+            work.wait()
 
     @property
     def frame(self):

@@ -16,9 +16,9 @@ import time
 
 import numpy as np
 
-from .core.tracing import Accumulator, as_image, render
+from .core.tracing import Accumulator, as_image, render_sums
 from .io_utils.read_tungsten import read_file
-from .tone_map import finish, reinhard_extended, to_uint8, write_png
+from .tone_map import finish, reinhard_extended, save_hdr, to_uint8, write_png
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DEFAULT_SCENE = os.path.join(HERE, "media", "cornell-box", "scene.json")
@@ -40,13 +40,16 @@ def parse(argv=None):
     ap.add_argument("--tonemap", choices=["sqrt", "reinhard"], default="sqrt",
                     help="finish() = sqrt(pixels/samples) (main_taichi.py:61-64) or finishing_tonemap (:67-78)")
     ap.add_argument("--out", default="out.png", help="PNG path ('' = no image)")
-    ap.add_argument("--hdr", help="also save the mean linear radiance (W, H, 3) [x][y] as .npy")
+    ap.add_argument("--hdr", metavar="DIR",
+                    help="also save the reference's HDR pair (main_taichi.py:120-123) into DIR: hdr.npy = the "
+                         "radiance sums (W, H, 3) [x][y], spp.npy = the per-pixel sample counts (W, H); "
+                         "the reference's tone_map.py reads exactly these")
     return ap.parse_args(argv)
 
 
-def _write(args, mean):
+def _write(args, sums, samples, mean):
     if args.hdr:
-        np.save(args.hdr, mean)
+        save_hdr(args.hdr, sums, samples)
     if args.out:
         img = finish(mean) if args.tonemap == "sqrt" else reinhard_extended(mean)
         write_png(args.out, to_uint8(as_image(img)))
@@ -84,13 +87,16 @@ def main(argv=None):
             print(f"{n / dt:.2f} samples/s ({acc.samples} spp, {W * H * n / dt / 1e6:.1f} Msamples/s)", flush=True)
             if state:
                 acc.save(state)
-        mean = acc.mean()
+        sums, samples, mean = acc.sums(), acc.samples, acc.mean()
         W, H = acc.W, acc.H
     else:
-        mean = render(scene, camera, spp=args.samples, depth=args.depth, seed=args.seed, resolution=(W, H),
-                      devices=tuple(args.devices), nee=args.nee)
+        sums = render_sums(scene, camera, spp=args.samples, depth=args.depth, seed=args.seed, resolution=(W, H),
+                           devices=tuple(args.devices), nee=args.nee)
+        samples = max(args.samples, 0)
+        # render()'s mean, bit for bit: pixels / samples (main_taichi.py:61-64)
+        mean = sums / np.float32(samples) if samples else np.zeros_like(sums)
     dt = time.perf_counter() - t0
-    _write(args, mean)
+    _write(args, sums, samples, mean)
     print(f"{W}x{H} x {args.samples} spp, depth {args.depth}: {dt:.2f} s "
           f"({W * H * args.samples / dt / 1e6:.1f} Msamples/s incl. scene build), mean RGB {mean.mean(axis=(0, 1))}")
     return mean

@@ -11,6 +11,28 @@ def finish(mean):
     return np.sqrt(np.asarray(mean, np.float32))
 
 
+def save_hdr(directory, sums, samples):
+    """The reference's HDR pair (main_taichi.py:120-123): `hdr.npy` = the per-pixel radiance SUMS
+    (`pixels.to_numpy()`, (W, H, 3) float32 [x][y]) and `spp.npy` = the per-pixel sample counts
+    (`samples.to_numpy()`, (W, H) float32), the input of the reference's offline tone_map.py:5-9.
+    Returns the two paths."""
+    import os
+    os.makedirs(directory, exist_ok=True)
+    sums = np.asarray(sums, np.float32)
+    hdr, spp = os.path.join(directory, "hdr.npy"), os.path.join(directory, "spp.npy")
+    np.save(hdr, sums)
+    np.save(spp, np.full(sums.shape[:2], np.float32(samples), np.float32))
+    return hdr, spp
+
+
+def finish_hdr(hdr_mat, spp_mat):
+    """tone_map.py:5-9 on the pair: NaN sums -> 0, then sqrt(hdr / spp[0, 0]) — finish() of the
+    mean (main_taichi.py:61-64) computed from the saved files."""
+    h = np.array(hdr_mat, np.float32)
+    h[np.isnan(h)] = 0
+    return np.sqrt(h / np.asarray(spp_mat, np.float32)[0, 0])
+
+
 def luminance(mean):
     """main_taichi.py:53-58 (NaN pixels skipped → 0)."""
     m = np.asarray(mean, np.float32)

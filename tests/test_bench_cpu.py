@@ -107,3 +107,17 @@ def test_mislaunch_exits_nonzero_before_any_gpu_call():
     assert r.returncode == 2 and "needs" in r.stderr and "visible" in r.stderr, r.stderr
     r = _run_bench(["--gpus", "0"])
     assert r.returncode == 2
+
+
+def test_ranks_sharing_a_gpu_are_refused_under_nccl():
+    """an N-GPU line must prove N distinct GPUs rendered.  bench.py gathers every
+    rank's (rank, local rank, device, PCI address) into config.ranks and refuses (exit 2) an nccl
+    launch whose ranks share a physical device; the gloo rehearsal may share one."""
+    r = [{"rank": 0, "local_rank": 0, "device": 0, "pci": "0000:05:00"},
+         {"rank": 1, "local_rank": 1, "device": 1, "pci": "0000:15:00"}]
+    assert bench.check_rank_devices(r, "nccl") is None
+    dup = [dict(r[0]), dict(r[1], device=0, pci="0000:05:00"), dict(r[1], rank=2, pci="0000:25:00")]
+    why = bench.check_rank_devices(dup, "nccl")
+    assert why and "0000:05:00" in why and "[0, 1]" in why
+    assert bench.check_rank_devices(dup, "gloo") is None
+    assert bench.shared_devices(dup) == {"0000:05:00": [0, 1]}

@@ -40,11 +40,22 @@ def test_bench_two_ranks_over_gloo_on_one_gpu():
     assert two["n_gpus"] == 2 and two["config"]["backend"] == "gloo"
     assert two["l2_vs_cpu"]["identical_pixels"] == 1.0 and two["l2_vs_cpu"]["pass"]
     assert two["value"] > 0 and two["steps"] == 2
+    # the line names the device of every rank and each rank's own step time
+    ranks = two["config"]["ranks"]
+    assert len(ranks) == 2 and sorted(r["rank"] for r in ranks) == [0, 1]
+    assert all(set(r) >= {"rank", "local_rank", "device", "pci", "uuid"} for r in ranks)
+    assert len({r["pci"] for r in ranks}) == 1          # gloo rehearsal: both ranks on the one GPU
+    rm = two["rank_ms_per_step"]
+    assert len(rm["per_rank"]) == 2 and 0 < rm["min"] <= rm["max"]
+    assert abs(rm["max"] - two["ms_per_step"]) <= 1e-3 * rm["max"] + 1e-3
+    # the one-frame-per-launch leg
+    sf = two["single_frame"]
+    assert sf["frames_per_launch"] == 1 and sf["ms_per_step"] > 0 and sf["kernel_avg_ms"] > 0
     r1 = subprocess.run([sys.executable, "bench.py"] + ARGS + ["--no-cpu-baseline"], cwd=ROOT, env=env,
                         capture_output=True, text=True, timeout=200)
     assert r1.returncode == 0, r1.stdout[-3000:] + r1.stderr[-3000:]
     one = _line(r1.stdout)
-    assert one["n_gpus"] == 1
+    assert one["n_gpus"] == 1 and len(one["config"]["ranks"]) == 1
     a, b = two["work_totals"], one["work_totals"]
     # path queries depend only on the (seed, pixel, sample) streams: exact for any tile split
     assert a["ext_queries"] == b["ext_queries"] and a["shadow_queries"] == b["shadow_queries"], (a, b)

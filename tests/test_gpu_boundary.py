@@ -92,10 +92,15 @@ def test_cli_progressive_resume_equals_one_render(tmp_path, cornell):
     common = ["--resolution", "48", "32", "--depth", "8", "--seed", "3"]
     main(common + ["--samples", "3", "--interval", "2", "--state", state, "--out", ""])
     mean = main(common + ["--samples", "6", "--interval", "2", "--state", state,
-                          "--out", str(tmp_path / "o.png"), "--hdr", str(tmp_path / "o.npy")])
+                          "--out", str(tmp_path / "o.png"), "--hdr", str(tmp_path / "hdr")])
     ref = render(cornell[0], cornell[1], spp=6, depth=8, seed=3, resolution=(48, 32))
     np.testing.assert_array_equal(mean, ref)
-    np.testing.assert_array_equal(np.load(tmp_path / "o.npy"), ref)
+    # the reference's HDR pair: radiance sums + per-pixel sample counts (main_taichi.py:120-123)
+    hdr, spp = np.load(tmp_path / "hdr" / "hdr.npy"), np.load(tmp_path / "hdr" / "spp.npy")
+    assert hdr.shape == (48, 32, 3) and spp.shape == (48, 32) and (spp == 6).all()
+    np.testing.assert_array_equal(hdr / spp[0, 0], ref)
+    m1 = main(common + ["--samples", "5", "--out", "", "--hdr", str(tmp_path / "one")])
+    np.testing.assert_array_equal(np.load(tmp_path / "one" / "hdr.npy") / np.float32(5), m1)
     assert (tmp_path / "o.png").read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"
     m2 = main(common + ["--samples", "2", "--nee", "mis", "--out", "", "--tonemap", "reinhard"])
     assert np.isfinite(m2).all() and not np.array_equal(m2, render(cornell[0], cornell[1], spp=2, depth=8, seed=3,
