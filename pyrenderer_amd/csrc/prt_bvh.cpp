@@ -158,7 +158,7 @@ struct Builder {
     int bins = 32;             // SAH bins per axis (env PRT_SAH_BINS, 2..64)
     double ct = 0.5;           // SAH cost of a node step relative to one triangle test (env PRT_SAH_CT)
     int leaf_min = 2;          // ranges of <= leaf_min triangles always become leaves (env PRT_LEAF_MIN)
-    bool sbvh = false;         // spatial splits (env PRT_SBVH=1; off by default)
+    bool sbvh = true;          // spatial splits (env PRT_SBVH=0 turns them off)
     double alpha = 1e-5;       // overlap threshold relative to the root's area (env PRT_SBVH_ALPHA)
     double min_overlap = 0.0;  // alpha x root area
     int64_t ref_budget = 0;    // spatial splits stop once the references reach this count
@@ -302,10 +302,13 @@ struct Builder {
                         bb[b0].grow(rb);
                         continue;
                     }
+                    // the search bins the reference box cut by the bin's slab (an upper bound of the
+                    // clipped triangle's bounds, exact for axis-aligned faces); the split itself clips
                     for (int k = b0; k <= b1; ++k) {
-                        Box part;
-                        const double pl = k == b0 ? -INFINITY : lo + w * k, ph = k == b1 ? INFINITY : lo + w * (k + 1);
-                        if (clip_ref(r, pl, ph, ax, &part)) bb[k].grow(part);
+                        Box part = rb;
+                        if (k > b0) part.lo[ax] = std::max(part.lo[ax], (float)(lo + w * k));
+                        if (k < b1) part.hi[ax] = std::min(part.hi[ax], (float)(lo + w * (k + 1)));
+                        bb[k].grow(part);
                     }
                 }
                 Box rbx[kMaxBins];
