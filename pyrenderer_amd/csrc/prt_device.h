@@ -384,6 +384,18 @@ struct LdsStack16 {
 // Pushes write the slot above the top unconditionally and advance the stack
 // pointer by the hit predicate (no exec-mask branches); the highest slot written
 // is the same as with conditional pushes (<= 3 above the entry top).
+// LDS-resident scene data (the block's octant node copies and triangles) addressed as LDS: the
+// element offset stays a 32-bit LDS address (v_mad_u32_u24 / v_lshl_add) instead of the 64-bit
+// flat-pointer arithmetic (v_mad_u64_u32) the generic pointer gets before address-space inference
+typedef float F4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const F4v LdsF4;
+__device__ __forceinline__ const LdsF4* as_lds(const float4* p) { return (const LdsF4*)p; }
+// one ds_read_b128 of element i
+__device__ __forceinline__ float4 lds4(const LdsF4* p, int i) {
+    const F4v v = p[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // Slab test from plane distances already ordered near/far (quantised nodes).
 __device__ __forceinline__ bool slab_t(float nx, float fx, float ny, float fy, float nz, float fz, float tmin,
                                        float tmax, float& tn) {
@@ -501,8 +513,17 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     } else {
         float4 nx, fx, ny, fy, nz, fz, rf;
         if (OCT) {
+#ifdef PRT_NO_LDS_ADDR32
             const float4* nd = nodes + (uint32_t)cur * 56u + sx;
+#else
+            const LdsF4* nl = as_lds(nodes) + (int)(__umul24((uint32_t)cur, 56u) + (uint32_t)sx);
+            auto nd = [&](int i) { return lds4(nl, i); };
+#endif
+#ifdef PRT_NO_LDS_ADDR32
             nx = nd[0]; fx = nd[1]; ny = nd[2]; fy = nd[3]; nz = nd[4]; fz = nd[5]; rf = nd[6];
+#else
+            nx = nd(0); fx = nd(1); ny = nd(2); fy = nd(3); nz = nd(4); fz = nd(5); rf = nd(6);
+#endif
         } else {
             // near/far planes picked by address (the node stores lo and hi per axis)
             const float4* nd = nodes + (size_t)cur * 8;
@@ -585,8 +606,9 @@ template <bool STATS>
 __device__ __forceinline__ void visit_oct_mixed(const float4* __restrict__ nodes, int& cur, int& sp, LdsStack16 st,
                                                 V3 inv, V3 oi, int sx, float tmin, float best, bool any,
                                                 Counters& cn) {
-    const float4* nd = nodes + (uint32_t)cur * 56u + sx;
-    const float4 nx = nd[0], fx = nd[1], ny = nd[2], fy = nd[3], nz = nd[4], fz = nd[5], rf = nd[6];
+    const LdsF4* nd = as_lds(nodes) + (int)(__umul24((uint32_t)cur, 56u) + (uint32_t)sx);
+    const float4 nx = lds4(nd, 0), fx = lds4(nd, 1), ny = lds4(nd, 2), fy = lds4(nd, 3), nz = lds4(nd, 4),
+                 fz = lds4(nd, 5), rf = lds4(nd, 6);
     if (STATS) { cn.nodes++; cn.it_inner++; }
     float t0, t1, t2, t3;
     const bool h0 = slab_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, oi, inv, tmin, best, t0);
@@ -653,8 +675,17 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
                 if (__builtin_amdgcn_readfirstlane(__lane_id()) == __lane_id()) cn.w_tri += mc;
             }
             for (int k = 0; k < cnt; ++k) {
-                const float4* tp = tris + (size_t)(first + k) * 3;
-                float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+                float4 q0, q1, q2;
+#ifndef PRT_NO_LDS_ADDR32
+                if constexpr (OCT) {
+                    const LdsF4* tp = as_lds(tris) + (int)__umul24((uint32_t)(first + k), 3u);
+                    q0 = lds4(tp, 0); q1 = lds4(tp, 1); q2 = lds4(tp, 2);
+                } else
+#endif
+                {
+                    const float4* tp = tris + (size_t)(first + k) * 3;
+                    q0 = tp[0]; q1 = tp[1]; q2 = tp[2];
+                }
                 int id = __float_as_int(q0.w);
                 float t;
                 if (STATS) { cn.tris++; wave_tick(cn.wl, cn.ll); }
@@ -1742,8 +1773,8 @@ void trace_kernel_pool(TraceParams P) {
                         const int v = -leaf - 1;
                         const int first = v >> 3, cnt = (v & 7) + 1;
                         for (int k = 0; k < cnt; ++k) {
-                            const float4* tp = g_tris + (size_t)(first + k) * 3;
-                            const float4 q0 = tp[0], q1 = tp[1], q2 = tp[2];
+                            const LdsF4* tp = as_lds(g_tris) + (int)__umul24((uint32_t)(first + k), 3u);
+                            const float4 q0 = lds4(tp, 0), q1 = lds4(tp, 1), q2 = lds4(tp, 2);
                             const int id = __float_as_int(q0.w);
                             float t;
                             if (STATS) { cn.tris++; wave_tick(cn.wl, cn.ll); }
