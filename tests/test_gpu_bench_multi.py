@@ -62,3 +62,22 @@ def test_bench_two_ranks_over_gloo_on_one_gpu():
     # node / triangle counts also depend on which lanes share a wave (leaf-phase thresholds)
     for k in ("nodes", "tris"):
         assert abs(a[k] - b[k]) <= 0.01 * b[k], (k, a, b)
+
+
+@pytest.mark.timeout(400)
+def test_bench_three_ranks_ragged_multi_frame_over_gloo():
+    """ADVICE r04 (medium) end to end: three gloo ranks on the one GPU, 64 tiles of 16 x 16 (ranks of
+    22 / 21 / 21 tiles: two ragged shards) and 4 frames per launch — the ranks render into their padded
+    gather rows at the slot pitch, rank 0 scatters the group in one launch; the gathered frame equals the
+    CPU oracle and the counters sum to the one-process counts."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    args = ["--res", "128", "--spp", "4", "--depth", "6", "--tile", "16", "--steps", "4", "--warmup", "1",
+            "--numpy-seconds", "0", "--cpu-seconds", "1", "--frames-per-launch", "4", "--single-frame-steps", "0"]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "3", "--backend", "gloo"] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    three = _line(r.stdout)
+    assert three["n_gpus"] == 3 and three["config"]["frames_per_launch"] == 4
+    assert len(three["config"]["ranks"]) == 3 and len(three["rank_ms_per_step"]["per_rank"]) == 3
+    assert three["l2_vs_cpu"]["identical_pixels"] == 1.0
