@@ -71,22 +71,32 @@ def _traverse_py(nodes, tris, order, ro, rd, tmin, tmax):
     return set(found)
 
 
-def test_bvh_build_is_a_partition_with_conservative_boxes():
+@pytest.mark.parametrize("sbvh", ["0", "1"])
+def test_bvh_build_covers_every_triangle_with_conservative_boxes(sbvh, monkeypatch):
+    """Object splits only (PRT_SBVH=0): the leaves partition the triangles and every leaf triangle lies
+    inside its child box.  With spatial splits (the default, prt_bvh.cpp) a triangle may have several
+    references, each bounding its part of the triangle: every triangle is referenced, and every point of
+    it lies inside the box of one of its references."""
     from pyrenderer_amd import _native as N
+    monkeypatch.setenv("PRT_SBVH", sbvh)
     rng = np.random.default_rng(3)
     n = 3000
     c = rng.uniform(-5, 5, (n, 1, 3))
     tv = (c + rng.normal(0, 0.2, (n, 3, 3))).astype(np.float32).reshape(n, 9)
     b = N.Bvh(tv, max_leaf=4)
     nodes, tris, order = b.export()
-    assert sorted(order.tolist()) == list(range(n))
+    if sbvh == "0":
+        assert sorted(order.tolist()) == list(range(n))
+    else:
+        assert set(order.tolist()) == set(range(n)) and n <= len(order) <= 1.3 * n + 1
     assert 1 <= b.depth <= 64
     # triangle records: v0 and f32 edges, original id in v0.w bits
     np.testing.assert_array_equal(tris[:, 0:3], tv[order, 0:3])
     np.testing.assert_array_equal(tris[:, 4:7], tv[order, 3:6] - tv[order, 0:3])
     np.testing.assert_array_equal(tris[:, 3].view(np.int32), order)
-    # every leaf triangle lies inside the child box that references it
+    # leaf boxes: whole triangles (object splits) / a cover of each triangle by its references' boxes
     import struct
+    boxes = {}
     for nd in nodes:
         for side in (0, 1):
             r = struct.unpack("<i", struct.pack("<f", nd[12 + side]))[0]
@@ -94,8 +104,17 @@ def test_bvh_build_is_a_partition_with_conservative_boxes():
                 v = -r - 1
                 first, cnt = v >> 3, (v & 7) + 1
                 bx = nd[6 * side:6 * side + 6]
-                pts = tv[order[first:first + cnt]].reshape(-1, 3)
-                assert np.all(pts >= np.array([bx[0], bx[2], bx[4]])) and np.all(pts <= np.array([bx[1], bx[3], bx[5]]))
+                lo, hi = np.array([bx[0], bx[2], bx[4]]), np.array([bx[1], bx[3], bx[5]])
+                for t in order[first:first + cnt]:
+                    boxes.setdefault(int(t), []).append((lo, hi))
+                if sbvh == "0":
+                    pts = tv[order[first:first + cnt]].reshape(-1, 3)
+                    assert np.all(pts >= lo) and np.all(pts <= hi)
+    w = rng.dirichlet((1, 1, 1), 12)
+    for t in range(0, n, 7):
+        v = tv[t].reshape(3, 3).astype(np.float64)
+        for p in np.concatenate([v, w @ v]):
+            assert any(np.all(p >= lo) and np.all(p <= hi) for lo, hi in boxes[t]), (t, p)
     # rays: the brute-force closest triangle is among the reachable leaves
     from oracle import oracle as O
     osc = O.OracleScene(tv, np.tile([0, 1, 0], (n, 1)), np.zeros(n), np.arange(n), tv[:, :3], tv[:, :3],
