@@ -40,7 +40,8 @@ extern "C" {
  * straight into a padded per-frame buffer; PRT_FLAG_NO_PRIMARY_KERNEL, accepted by ABI 2, is
  * rejected with PRT_ERR_UNSUP; prt_scatter_frames and prt_camera_rays added; variant ids 9 / 10 (the pooled kernel's
  * fused schedule, 7 / 6 waves per SIMD: extension traversals also answer the pooled shadow rays)
- * added, ids above 10 rejected with PRT_ERR_ARG. */
+ * and 11 / 12 (the pooled kernel with packed leaf trips) added, ids above 12 rejected with
+ * PRT_ERR_ARG. */
 #define PRT_ABI_VERSION 3
 
 #define PRT_OK 0
@@ -70,7 +71,8 @@ extern "C" {
  * SIMD), 2 the same without an occupancy target, 3 global scene (quantised nodes, spill
  * stack), 4 / 5 the MIS estimator on an LDS / global scene, 6 the LDS-resident scene built
  * for >= 6 waves per SIMD, 7 / 8 the LDS-resident block-pooled shadow kernel for >= 7 / >= 6
- * waves per SIMD).  Variants of one estimator produce
+ * waves per SIMD, 9 / 10 its fused schedule, 11 / 12 it with packed leaf trips).  Variants of one
+ * estimator produce
  * bit-identical images; the selector exists for A/B runs and tests. */
 #define PRT_FLAG_VARIANT_SHIFT 8
 #define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFFu) << PRT_FLAG_VARIANT_SHIFT)

@@ -1490,6 +1490,168 @@ __device__ __forceinline__ void copy_octant_nodes(float4* __restrict__ sn, const
     }
 }
 
+// ------------------------------------------------ packed leaf phase (round 5, PRT_PACK variants)
+// A wave's while-while traversal spends most of its triangle-test trips with few lanes busy
+// (lane table, config 2: 0.29): every lane tests its own leaf one triangle per trip, so a trip
+// count is the wave's LONGEST leaf while most lanes hold short ones or none.  traverse_pk tests
+// the (lane, triangle) pairs of all the leaves the wave's lanes hold 64 to a trip instead: pair p
+// goes to lane p mod 64 of trip p / 64, which fetches the owner's ray and bound from the owner's
+// registers (ds_bpermute), tests the triangle, and the owner folds its pairs' results back in —
+// any-hit: one ballot; closest-hit: a (t, id) minimum over the owner's run of lanes.  The result of
+// a query is the lexicographic minimum (t, id) over its triangle hits whatever the order of the
+// tests (any-hit: whether one exists), so images stay bit-identical.
+constexpr int kPkF4 = 4 * 64 / 16;   // LDS: 64 owner bytes per wave
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int bperm(int src_lane, int v) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
+__device__ __forceinline__ float bperm(int src_lane, float v) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
+}
+// inclusive prefix maximum over the wave: DPP row shifts within each 16-lane row, then the row
+// broadcasts of lanes 15 and 31 (lanes a shift reaches from outside keep the identity)
+__device__ __forceinline__ int wave_max_scan(int v) {
+    constexpr int kId = (int)0x80000000;
+    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return v;
+}
+
+// While-while traversal of the LDS octant BVH4 with packed leaf trips.  Called by ALL 64 lanes of
+// the wave (act: this lane has a query); NP: leaves a lane may hold (postponed) before it stops
+// descending — the leaf phase tests all of them in one round.  wb: the wave's 64 owner bytes.
+// Leaf references of an LDS scene are 16-bit (first < 4096), so two held leaves share a word.
+template <bool STATS, bool ANY, int NP>
+__device__ __forceinline__ bool traverse_pk(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
+                                            V3 d, float tmax, bool act, LdsStack16 stk, int8_t* wb, int& hit_id,
+                                            float& hit_t, Counters& cn, int* fault, int lb, int le,
+                                            uint32_t guard_lim) {
+    static_assert(NP >= 1 && NP <= 3, "held leaves");
+    const int lane = (int)__lane_id();
+    const V3 inv = ray_inv(d);
+    const V3 oi = o * inv;
+    const int sx = 7 * ((__float_as_int(inv.x) < 0 ? 1 : 0) | (__float_as_int(inv.y) < 0 ? 2 : 0) |
+                        (__float_as_int(inv.z) < 0 ? 4 : 0));
+    stk.put(0, LdsStack16::kSent);
+    int cur = act ? root_for<LdsStack16>(tmax) : LdsStack16::kSent;
+    int sp = 0;
+    float best = tmax;
+    int best_id = -1;
+    bool found = false;
+    // held leaves (first << 3 | count - 1): h01 = leaf 0 | leaf 1 << 16, h2 = leaf 2; nh of them
+    uint32_t h01 = 0, h2 = 0;
+    int nh = 0;
+    auto hold = [&]() {
+        if (cur < 0 && nh == 0) { h01 = (uint32_t)(-cur - 1); nh = 1; cur = stk.get(sp); --sp; }
+        if (NP >= 2 && cur < 0 && nh == 1) { h01 |= (uint32_t)(-cur - 1) << 16; nh = 2; cur = stk.get(sp); --sp; }
+        if (NP >= 3 && cur < 0 && nh == 2) { h2 = (uint32_t)(-cur - 1); nh = 3; cur = stk.get(sp); --sp; }
+    };
+    uint32_t guard = 0;
+    while (true) {
+        // inner phase: descend until at most lb of the descending lanes hold no leaf
+        while (cur >= 0 && cur != LdsStack16::kSent && nh < NP) {
+            visit_node4<STATS, ANY ? 2 : 1, LdsStack16, false, true>(nodes, cur, sp, stk, inv, oi, sx, 0, 0, kTMin,
+                                                                    best, cn);
+            if (STATS) {
+                wave_tick(cn.wi, cn.li);
+                cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
+            }
+            hold();
+            if (__popcll(__ballot(nh == 0)) <= (uint32_t)lb) break;
+        }
+        // leaf rounds (wave-uniform): every held leaf of every lane, 64 pairs per trip
+        while (__ballot(nh > 0) != 0) {
+            const uint32_t v0 = h01 & 0xFFFFu, v1 = h01 >> 16;
+            const int c = (nh > 0 ? (int)(v0 & 7u) + 1 : 0) + (nh > 1 ? (int)(v1 & 7u) + 1 : 0) +
+                          (nh > 2 ? (int)(h2 & 7u) + 1 : 0);   // pairs of this lane, <= 8 NP
+            // exclusive prefix of c over the lanes and the round's total, by bit planes
+            uint32_t pre = 0, total = 0;
+            int steps = 0;   // reduction steps covering the longest run (< 2^steps)
+#pragma unroll
+            for (int b = 0; b < 5; ++b) {
+                const uint64_t m = __ballot((c >> b) & 1);
+                pre += lane_rank(m) << b;
+                total += (uint32_t)__popcll(m) << b;
+                steps = m ? b + 1 : steps;
+            }
+            int carry = -1;
+            for (uint32_t base = 0; base < total; base += 64u) {
+                // owner of pair base + lane: owners mark where their run starts, then a prefix max
+                // (owners ascend with the pair index) fills the runs
+                wb[lane] = (int8_t)-1;
+                if (c > 0 && pre >= base && pre < base + 64u) wb[pre - base] = (int8_t)lane;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const int owner = wave_max_scan(max((int)wb[lane], carry));
+                carry = __builtin_amdgcn_readlane(owner, 63);
+                const bool valid = base + (uint32_t)lane < total;
+                const V3 qo = v3(bperm(owner, o.x), bperm(owner, o.y), bperm(owner, o.z));
+                const V3 qd = v3(bperm(owner, d.x), bperm(owner, d.y), bperm(owner, d.z));
+                const float ob = bperm(owner, best);
+                const int obid = ANY ? -1 : bperm(owner, best_id);
+                const int opre = bperm(owner, (int)pre), oc = bperm(owner, c);
+                const uint32_t oh01 = (uint32_t)bperm(owner, (int)h01);
+                const uint32_t oh2 = NP >= 3 ? (uint32_t)bperm(owner, (int)h2) : 0u;
+                const int k = (int)(base + (uint32_t)lane) - opre;   // pair k of the owner's run
+                const uint32_t ov0 = oh01 & 0xFFFFu, ov1 = oh01 >> 16;
+                const int oc0 = (int)(ov0 & 7u) + 1, oc1 = (int)(ov1 & 7u) + 1;
+                int ti = k < oc0 ? (int)(ov0 >> 3) + k
+                         : (NP < 3 || k < oc0 + oc1) ? (int)(ov1 >> 3) + (k - oc0)
+                                                     : (int)(oh2 >> 3) + (k - oc0 - oc1);
+                ti = valid ? ti : 0;
+                const LdsF4* tp = as_lds(tris) + (int)__umul24((uint32_t)ti, 3u);
+                const float4 q0 = lds4(tp, 0), q1 = lds4(tp, 1), q2 = lds4(tp, 2);
+                const int id = __float_as_int(q0.w);
+                float t;
+                const bool h = mt_u(xyz(q0), xyz(q1), xyz(q2), qo, qd, kTMin, ob, id, obid, ANY, t) & valid;
+                if (STATS) {
+                    cn.tris += valid ? 1u : 0u;
+                    const uint64_t vm = __ballot(valid);
+                    if (lane == 0) { cn.wl += 1u; cn.ll += (uint32_t)__popcll(vm); cn.it_leaf++; }
+                }
+                // this lane's own run within the trip: lanes [lo, hi)
+                const int lo = max((int)pre - (int)base, 0), hi = min((int)(pre + (uint32_t)c) - (int)base, 64);
+                const bool mine = c > 0 && lo < hi;
+                if (ANY) {
+                    const uint64_t hm = __ballot(h);
+                    const uint64_t span = (hi - lo >= 64) ? ~0ull : ((1ull << (hi - lo)) - 1ull);
+                    if (mine && ((hm >> lo) & span) != 0) found = true;
+                } else {
+                    // (t, id) minimum over the owner's run, toward its first lane: misses are ~0
+                    uint32_t kt = h ? __float_as_uint(t) : 0xFFFFFFFFu, ki = h ? (uint32_t)id : 0xFFFFFFFFu;
+                    const int send = min(opre + oc - (int)base, 64);   // end of the run this lane is in
+                    for (int s = 1, j = 0; j < steps; s <<= 1, ++j) {
+                        const uint32_t at = (uint32_t)bperm(lane + s, (int)kt), ai = (uint32_t)bperm(lane + s, (int)ki);
+                        const bool take = (lane + s < send) & ((at < kt) | ((at == kt) & (ai < ki)));
+                        kt = take ? at : kt;
+                        ki = take ? ai : ki;
+                    }
+                    const uint32_t rt = (uint32_t)bperm(lo, (int)kt), ri = (uint32_t)bperm(lo, (int)ki);
+                    if (mine && ri != 0xFFFFFFFFu) { best = __uint_as_float(rt); best_id = (int)ri; }
+                }
+            }
+            nh = 0; h01 = 0; h2 = 0;
+            if (ANY && found) cur = LdsStack16::kSent;
+            hold();
+            if (__popcll(__ballot(nh > 0)) <= (uint32_t)le) break;
+        }
+        // watchdog (traverse_ww4's)
+        if (++guard > guard_lim) {
+            if (fault && lane == 0) atomicOr(fault, 1);
+            cur = LdsStack16::kSent;
+            nh = 0;
+        }
+        if (__ballot(cur != LdsStack16::kSent || nh > 0) == 0) break;
+    }
+    hit_id = best_id;
+    hit_t = best;
+    return ANY ? found : best_id >= 0;
+}
+
 // Block-pooled shadow queries (LDS-resident scenes, the reference estimator).
 //
 // trace_kernel's phase-aligned waves alternate an extension iteration (62.5 of 64 lanes query at
@@ -1536,9 +1698,12 @@ constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 
 // PLAIN: the lean build for scenes without spheres and metal / dielectric materials (P.plain; C1, C2,
 // C5): without that code the kernel's loop keeps 17 fewer uniform values in spilled SGPRs and is a
 // third shorter
-template <bool STATS, int WPE, bool PLAIN, bool FUSED>
+// PK (round 5, variants 11 / 12): the two-phase schedule with packed leaf trips (traverse_pk, PK held
+// leaves per lane) in the extension and the shadow traversals
+template <bool STATS, int WPE, bool PLAIN, bool FUSED, int PK = 0>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel_pool(TraceParams P) {
+    static_assert(!(FUSED && PK), "one schedule");
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1548,7 +1713,8 @@ void trace_kernel_pool(TraceParams P) {
     float* pool = reinterpret_cast<float*>(smem + stack_f4);   // [7][256]
     uint8_t* queue = reinterpret_cast<uint8_t*>(smem + stack_f4 + kPoolF4);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + stack_f4 + kPoolF4 + kQueueF4);
-    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + kCtlF4;
+    int8_t* wb = reinterpret_cast<int8_t*>(smem + stack_f4 + kPoolF4 + kQueueF4 + kCtlF4) + (tid & ~63);
+    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + kCtlF4 + (PK ? kPkF4 : 0);
     const int n_node4 = P.n_node_f4 / 8;
     float4* st4 = sn + 56 * n_node4;
     float4* slv = st4 + P.n_tri_f4;
@@ -1845,12 +2011,24 @@ void trace_kernel_pool(TraceParams P) {
             d = wi;
         } else if (__ballot(trav) != 0) {
             if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_e++;
+            if constexpr (PK != 0) {
+                // packed leaf trips: every lane of the wave takes part (lanes without a query test
+                // the others' triangles)
+                if (STATS && trav) { cn.ext++; cn.q0 = cn.nodes; }
+                hit = traverse_pk<STATS, false, PK>(g_nodes, g_tris, o, d, kTMax, trav, stk, wb, hid, ht, cn, P.fault,
+                                                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit,
+                                                    P.guard_trips) &&
+                      trav;
+                if (STATS) { if (trav) cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
+            }
             if (trav) {
-                if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
-                hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
-                    g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
-                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
+                if constexpr (PK == 0) {
+                    if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
+                    hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
+                        g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
+                        exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                    if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
+                }
                 if (!PLAIN && P.n_sph > 0) {
                     float best = hit ? ht : kTMax;
                     for (int k = 0; k < P.n_sph; ++k) {
@@ -2083,18 +2261,37 @@ void trace_kernel_pool(TraceParams P) {
             const uint32_t e0 = chunk * 64u, e1 = min(n_q, e0 + 64u);
             const uint32_t e = e0 + (uint32_t)lane;
             if (STATS && lane == 0) { n_s++; lanes_s += e1 - e0; }
-            if (e < e1) {
-                const int owner = queue[qpar * kBlock + e];
-                const V3 so = v3(pool[0 * kBlock + owner], pool[1 * kBlock + owner], pool[2 * kBlock + owner]);
-                const V3 sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
-                const float stm = pool[6 * kBlock + owner];
+            const bool sq = e < e1;
+            int owner = 0;
+            V3 so = v3(0, 0, 0), sd = v3(1, 1, 1);
+            float stm = 0.0f;
+            if (sq) {
+                owner = queue[qpar * kBlock + e];
+                so = v3(pool[0 * kBlock + owner], pool[1 * kBlock + owner], pool[2 * kBlock + owner]);
+                sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
+                stm = pool[6 * kBlock + owner];
+            }
+            bool s_hit = false;
+            if constexpr (PK != 0) {
                 int hid = -1;
                 float ht = 0.0f;
                 if (STATS) cn.q0 = cn.nodes;
-                bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
-                    g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
-                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
+                s_hit = traverse_pk<STATS, true, PK>(g_nodes, g_tris, so, sd, stm, sq, stk, wb, hid, ht, cn, P.fault,
+                                                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit,
+                                                     P.guard_trips);
+                if (STATS) { if (sq) cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
+            }
+            if (sq) {
+                int hid = -1;
+                float ht = 0.0f;
+                bool hit = s_hit;
+                if constexpr (PK == 0) {
+                    if (STATS) cn.q0 = cn.nodes;
+                    hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
+                        g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
+                        exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                    if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
+                }
                 if (!PLAIN && P.n_sph > 0 && !hit) {
                     for (int k = 0; k < P.n_sph; ++k) {
                         float root;
@@ -2179,7 +2376,12 @@ void trace_kernel_pool(TraceParams P) {
     X(kVarLdsPool, 512, true, 7)              \
     X(kVarLdsPool6, 512, true, 6)             \
     X(kVarLdsFused, 1536, true, 7)            \
-    X(kVarLdsFused6, 1536, true, 6)
+    X(kVarLdsFused6, 1536, true, 6)           \
+    X(kVarLdsPack, 2560, true, 7)             \
+    X(kVarLdsPack6, 2560, true, 6)
+
+// the pool kernel's schedule of a variant's bits: 1024 FUSED, 2048 packed leaf trips
+constexpr int pool_sched(int bits) { return (bits & 1024) ? kPoolFused : (bits & 2048) ? kPoolPacked : kPoolTwoPhase; }
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
@@ -2188,7 +2390,7 @@ static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStr
     if constexpr ((VAR & 512) != 0) {
         // the pool kernel's LDS stack size is a launch parameter (P.lds_stack): one instantiation,
         // compiled in its own unit (prt_trace_pool.hip, other register-allocation flags)
-        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, (VAR & 1024) != 0, grid, smem, stream);
+        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, pool_sched(VAR), grid, smem, stream);
         else return hipErrorInvalidValue;
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
         trace_kernel<STACK, STATS, VAR, LDS, WPE><<<grid, kBlock, smem, stream>>>(P);
@@ -2213,7 +2415,7 @@ template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
 static void occ_one(int* n, size_t smem) {
     constexpr bool spill = (VAR & 32) != 0;
     if constexpr ((VAR & 512) != 0) {
-        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, (VAR & 1024) != 0, smem);
+        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, pool_sched(VAR), smem);
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(n, trace_kernel<STACK, STATS, VAR, LDS, WPE>, kBlock, smem);
 }

@@ -81,9 +81,15 @@ constexpr int kVarLdsPool6 = 8;    // kVarLdsPool built for >= 6 waves/SIMD (80 
 constexpr int kVarLdsFused = 9;    // trace_kernel_pool FUSED (round 5): the extension traversals' idle lanes
                                    // answer the previous iteration's pooled shadow rays; no S phase
 constexpr int kVarLdsFused6 = 10;  // kVarLdsFused built for >= 6 waves/SIMD
+constexpr int kVarLdsPack = 11;    // trace_kernel_pool, two-phase, packed leaf trips (round 5): the triangle
+                                   // tests of all leaves the wave's lanes hold run 64 to a trip (traverse_pk)
+constexpr int kVarLdsPack6 = 12;   // kVarLdsPack built for >= 6 waves/SIMD
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 10;
+constexpr int kVarLast = 12;
+// trace_kernel_pool schedules
+constexpr int kPoolTwoPhase = 0, kPoolFused = 1, kPoolPacked = 2;
 bool variant_pool(int var);
+bool variant_pack(int var);
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
@@ -120,9 +126,10 @@ hipError_t launch_scatter_frames(const float* packed, const uint32_t* tile_xy, i
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 // the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
 // the pooled kernel's lean instantiation (no sphere or specular code) runs when P.plain is set
-// (fused: the schedule whose extension traversals also answer the previous iteration's shadow rays)
-hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, bool fused, int grid, size_t smem,
+// (sched: kPoolTwoPhase; kPoolFused, whose extension traversals also answer the previous iteration's
+// shadow rays; kPoolPacked, two-phase with packed leaf trips)
+hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int sched, int grid, size_t smem,
                              hipStream_t stream);
-int trace_occ_pool(bool stats, int wpe, bool fused, size_t smem);
+int trace_occ_pool(bool stats, int wpe, int sched, size_t smem);
 
 }  // namespace prt

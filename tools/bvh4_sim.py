@@ -2,7 +2,8 @@
 octant copies) simulated on the CPU for waves of 64 extension rays (round 5, profiles/r05/coherence_sim/):
 the leaf-buffering depth (npost: leaves a lane may hold before it stops descending; the kernels' "leaf +
 cur" is 2) and the leaf-phase entry / exit thresholds (lb / le, the kernels' PRT_LEAF_BREAK / PRT_LEAF_EXIT),
-priced with the per-trip VALU counts of the pooled kernel's ISA (79 per node visit, 73 per triangle test).
+priced with the per-trip VALU counts of the pooled kernel's ISA (79 per node visit, 73 per triangle test),
+and the packed leaf trips of traverse_pk (every held leaf's triangles 64 to a trip).
 The greedy collapse stands in for the build's SAH-optimal one (3.44 vs 3.17 node visits per query); at
 npost 2 the lane fractions match the GPU lane table (0.463 / 0.269 against 0.444 / 0.294).
 
@@ -86,7 +87,10 @@ class Sim:
         else:
             st['cur'][j] = st['stk'][j].pop()
 
-    def wave(self, queries, lb=0, le=8, npost=1):
+    def wave(self, queries, lb=0, le=8, npost=1, packed=False):
+        """Trip counts of one wave: (inner trips, inner lanes, triangle trips, triangle lanes, leaf rounds).
+        packed: a leaf round tests the (lane, triangle) pairs of every held leaf 64 to a trip
+        (traverse_pk, round 5) against each lane's bound at the round's start."""
         n = len(queries)
         st = {'o': [None]*n, 'd': [None]*n, 'inv': [None]*n, 'best': [0.0]*n, 'any': [False]*n,
               'cur': [SENT]*n, 'leaves': [[] for _ in range(n)], 'stk': [[SENT] for _ in range(n)], 'qi': [0]*n}
@@ -96,7 +100,7 @@ class Sim:
             st['inv'][j] = 1.0 / np.where(q[1] == 0, 1e-30, q[1])
             st['cur'][j], st['leaves'][j], st['stk'][j] = 0, [], [SENT]
         def active(j): return not (st['cur'][j] == SENT and not st['leaves'][j])
-        wi = li = wl = ll = 0
+        wi = li = wl = ll = rounds = 0
         while True:
             for j in range(n):
                 if not active(j) and st['qi'][j] < len(queries[j]): start(j)
@@ -113,6 +117,7 @@ class Sim:
             while True:
                 lanes = [j for j in range(n) if st['leaves'][j]]
                 if not lanes: break
+                rounds += 1
                 work = {}
                 for j in lanes:
                     tl = []
@@ -120,7 +125,16 @@ class Sim:
                         v = -lf - 1; tl += list(range(v >> 3, (v >> 3) + (v & 7) + 1))
                     work[j] = tl
                 done_any = set()
-                for k in range(max(len(w) for w in work.values())):
+                if packed:
+                    P = sum(len(w) for w in work.values())
+                    wl += -(-P // 64); ll += P
+                    for j in lanes:
+                        b0 = st['best'][j]
+                        ts = [t for t in (self.tri(k, st['o'][j], st['d'][j], b0) for k in work[j]) if t is not None]
+                        if ts:
+                            st['best'][j] = min(ts)
+                            if st['any'][j]: done_any.add(j)
+                for k in range(0 if packed else max(len(w) for w in work.values())):
                     act = [j for j in lanes if k < len(work[j]) and j not in done_any]
                     if not act: break
                     wl += 1; ll += len(act)
@@ -135,7 +149,7 @@ class Sim:
                     while st['cur'][j] != SENT and st['cur'][j] < 0 and len(st['leaves'][j]) < npost:
                         st['leaves'][j].append(st['cur'][j]); st['cur'][j] = st['stk'][j].pop()
                 if sum(1 for j in range(n) if st['leaves'][j]) <= le: break
-        return wi, li, wl, ll
+        return wi, li, wl, ll, rounds
 
 if __name__ == "__main__":
     flat, cam, n4, orders, T = load()
@@ -144,15 +158,21 @@ if __name__ == "__main__":
     rng = np.random.default_rng(0)
     O_, D_, B = bounce_rays(flat, cam, 20000, rng)
     perm = rng.permutation(len(O_))[:64 * 150]
-    def run(label, **kw):
-        wi = li = wl = ll = 0
+    def run(label, X=30, Y=25, **kw):
+        """X / Y: extra VALU per packed trip (owner scan, (t, id) reduction) / per packed round (prefix sums)"""
+        wi = li = wl = ll = rr = 0
         for g in range(0, len(perm), 64):
             r = sim.wave([[(O_[i], D_[i], 99999.9, False)] for i in perm[g:g + 64]], **kw)
-            wi, li, wl, ll = wi + r[0], li + r[1], wl + r[2], ll + r[3]
+            wi, li, wl, ll, rr = wi + r[0], li + r[1], wl + r[2], ll + r[3], rr + r[4]
         nq = len(perm)
-        cost = (wi * 79 + wl * 73) / (nq / 64)
+        pk = kw.get("packed", False)
+        cost = (wi * 79 + wl * (73 + (X if pk else 0)) + (rr * Y if pk else 0)) / (nq / 64)
         print(f"{label:28s} inner trips/wave {wi/(nq/64):.2f} lanes {li/(64*wi):.3f} | tri trips/wave {wl/(nq/64):.2f} lanes {ll/(64*wl):.3f} | visits/ray {li/nq:.2f} tests/ray {ll/nq:.2f} | VALU/wave {cost:.0f}", flush=True)
     print("---")
     for npost in (2, 3, 4):
         for lb, le in ((0, 8), (4, 8), (8, 8), (0, 16), (8, 16)):
             run(f"npost {npost} lb{lb} le{le}", npost=npost, lb=lb, le=le)
+    print("--- packed leaf trips (traverse_pk): 30 extra VALU per trip, 25 per round")
+    for npost in (1, 2, 3, 4):
+        for lb, le in ((0, 0), (0, 8), (4, 8)):
+            run(f"packed npost {npost} lb{lb} le{le}", npost=npost, lb=lb, le=le, packed=True)
