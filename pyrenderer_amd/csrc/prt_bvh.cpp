@@ -421,6 +421,126 @@ struct Builder {
 
 inline float bits_f(int32_t v) { float f; std::memcpy(&f, &v, 4); return f; }
 
+// Treelet restructuring (Karras & Aila 2013, "Fast Parallel Construction of High-Quality Bounding
+// Volume Hierarchies" §4): bottom-up, each inner node and its descendants down to 7 subtrees (the
+// largest-area subtree expanded first) form a treelet whose binary topology over those 7 subtrees
+// is replaced by the SAH-optimal one (a dynamic program over the 127 subsets), reusing the
+// treelet's inner nodes.  Leaves and the references they hold are unchanged, so the leaf order
+// and the triangle records stay valid; only inner boxes and child links move.  SAH cost of a
+// subtree: leaf area x references, inner node ct x area + its children's costs.
+void restructure_treelets(std::vector<TNode>& nodes, int32_t root, double ct, int passes) {
+    constexpr int kT = 7;
+    std::vector<double> cost(nodes.size(), 0.0);
+    std::vector<int32_t> post;
+    std::vector<std::pair<int32_t, bool>> st;
+    double box_a[1 << kT];
+    Box box_m[1 << kT];
+    double copt[1 << kT];
+    int part[1 << kT];
+    for (int pass = 0; pass < passes; ++pass) {
+        post.clear();
+        st.assign(1, {root, false});
+        while (!st.empty()) {
+            const auto [t, done] = st.back();
+            st.pop_back();
+            if (done || nodes[t].count > 0) { post.push_back(t); continue; }
+            st.push_back({t, true});
+            st.push_back({nodes[t].right, false});
+            st.push_back({nodes[t].left, false});
+        }
+        int64_t changed = 0;
+        for (int32_t t : post) {
+            TNode& nd = nodes[t];
+            if (nd.count > 0) { cost[t] = nd.box.area() * nd.count; continue; }
+            int32_t lv[kT] = {nd.left, nd.right};
+            int32_t inner[kT];
+            int nl = 2, ni = 0;
+            double old = ct * nd.box.area();
+            while (nl < kT) {
+                int j = -1;
+                double best_a = -1.0;
+                for (int i = 0; i < nl; ++i)
+                    if (nodes[lv[i]].count == 0 && nodes[lv[i]].box.area() > best_a) { best_a = nodes[lv[i]].box.area(); j = i; }
+                if (j < 0) break;
+                const int32_t x = lv[j];
+                inner[ni++] = x;
+                old += ct * best_a;
+                lv[j] = nodes[x].left;
+                lv[nl++] = nodes[x].right;
+            }
+            for (int i = 0; i < nl; ++i) old += cost[lv[i]];
+            if (nl < 3) { cost[t] = old; continue; }
+            const int full = (1 << nl) - 1;
+            for (int m = 1; m <= full; ++m) {
+                const int low = m & -m;
+                if (m == low) {
+                    const int i = __builtin_ctz((unsigned)m);
+                    box_m[m] = nodes[lv[i]].box;
+                    copt[m] = cost[lv[i]];
+                    continue;
+                }
+                box_m[m] = box_m[m ^ low];
+                box_m[m].grow(box_m[low]);
+                box_a[m] = box_m[m].area();
+                double best = DBL_MAX;
+                int bp = 0;
+                // partitions {sub, m ^ sub} with the lowest subtree in sub (each split once)
+                for (int sub = (m - 1) & m; sub; sub = (sub - 1) & m) {
+                    if (!(sub & low)) continue;
+                    const double c = copt[sub] + copt[m ^ sub];
+                    if (c < best) { best = c; bp = sub; }
+                }
+                copt[m] = ct * box_a[m] + best;
+                part[m] = bp;
+            }
+            if (!(copt[full] < old * (1.0 - 1e-12))) { cost[t] = old; continue; }
+            // rebuild the treelet below t with the optimal splits, reusing its inner nodes
+            int used = 0;
+            std::vector<std::pair<int32_t, int>> todo{{t, full}};
+            while (!todo.empty()) {
+                const auto [id, m] = todo.back();
+                todo.pop_back();
+                const int a = part[m], b = m ^ part[m];
+                int32_t kids[2];
+                const int ms[2] = {a, b};
+                for (int s = 0; s < 2; ++s) {
+                    if ((ms[s] & (ms[s] - 1)) == 0) {
+                        kids[s] = lv[__builtin_ctz((unsigned)ms[s])];
+                    } else {
+                        const int32_t nid = inner[used++];
+                        nodes[nid].box = box_m[ms[s]];
+                        nodes[nid].count = 0;
+                        cost[nid] = copt[ms[s]];
+                        todo.push_back({nid, ms[s]});
+                        kids[s] = nid;
+                    }
+                }
+                nodes[id].left = kids[0];
+                nodes[id].right = kids[1];
+            }
+            cost[t] = copt[full];
+            ++changed;
+        }
+        if (std::getenv("PRT_BVH_VERBOSE"))
+            std::fprintf(stderr, "prt_bvh: treelet pass %d: %lld treelets restructured, SAH %.3f\n", pass,
+                         (long long)changed, nodes[root].box.area() > 0 ? cost[root] / nodes[root].box.area() : 0.0);
+        if (!changed) break;
+    }
+}
+
+// depth of the deepest node below `root` (root = 0), as Builder::build counts it
+int32_t tree_depth(const std::vector<TNode>& nodes, int32_t root) {
+    int32_t d = 0;
+    std::vector<std::pair<int32_t, int32_t>> st{{root, 0}};
+    while (!st.empty()) {
+        const auto [t, k] = st.back();
+        st.pop_back();
+        d = std::max(d, k);
+        if (nodes[t].count == 0) { st.push_back({nodes[t].left, k + 1}); st.push_back({nodes[t].right, k + 1}); }
+    }
+    return d;
+}
+
 }  // namespace
 
 bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, std::string* err) {
@@ -507,6 +627,16 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
         B.nodes.reserve((size_t)(2 * n_ref0 / std::max(1, max_leaf / 2) + 8));
         if (scene.valid()) B.min_overlap = B.alpha * scene.area();
         root = B.build(all, 0);
+        // treelet restructuring passes (env PRT_TREELET, 0 = off): on by default for scenes of >= 2^14
+        // triangles (config 4: BVH2 SAH -3 %, node visits -2.1 %, 157.5 -> 154.6 ms per launch); the
+        // small LDS-resident scenes keep the plain tree, whose BVH4 collapse visits fewer nodes there
+        // (Cornell: 22.7 vs 26.3 node visits per sample with the restructured tree, profiles/r05/treelet/)
+        int passes = n_tri >= (1 << 14) ? 3 : 0;
+        if (const char* e = std::getenv("PRT_TREELET")) passes = std::max(0, std::min(8, std::atoi(e)));
+        if (passes > 0 && B.nodes[root].count == 0) {
+            restructure_treelets(B.nodes, root, B.ct, passes);
+            B.max_depth = tree_depth(B.nodes, root);
+        }
     }
     // every reference sits in exactly one leaf: the leaf order is the triangle records' order
     const int64_t n_ref = (int64_t)B.order.size();

@@ -71,19 +71,24 @@ def _traverse_py(nodes, tris, order, ro, rd, tmin, tmax):
     return set(found)
 
 
-@pytest.mark.parametrize("sbvh", ["0", "1"])
-def test_bvh_build_covers_every_triangle_with_conservative_boxes(sbvh, monkeypatch):
+@pytest.mark.parametrize("sbvh,treelet", [("0", "0"), ("1", "0"), ("1", "3"), ("0", "3")])
+def test_bvh_build_covers_every_triangle_with_conservative_boxes(sbvh, treelet, monkeypatch):
     """Object splits only (PRT_SBVH=0): the leaves partition the triangles and every leaf triangle lies
     inside its child box.  With spatial splits (the default, prt_bvh.cpp) a triangle may have several
     references, each bounding its part of the triangle: every triangle is referenced, and every point of
-    it lies inside the box of one of its references."""
+    it lies inside the box of one of its references.  Treelet restructuring (PRT_TREELET passes) only
+    rearranges inner nodes: the same guarantees hold, and the SAH cost does not rise."""
     from pyrenderer_amd import _native as N
     monkeypatch.setenv("PRT_SBVH", sbvh)
+    monkeypatch.setenv("PRT_TREELET", treelet)
     rng = np.random.default_rng(3)
     n = 3000
     c = rng.uniform(-5, 5, (n, 1, 3))
     tv = (c + rng.normal(0, 0.2, (n, 3, 3))).astype(np.float32).reshape(n, 9)
     b = N.Bvh(tv, max_leaf=4)
+    if treelet != "0":
+        monkeypatch.setenv("PRT_TREELET", "0")
+        assert b.sah_cost <= N.Bvh(tv, max_leaf=4).sah_cost + 1e-9
     nodes, tris, order = b.export()
     if sbvh == "0":
         assert sorted(order.tolist()) == list(range(n))
