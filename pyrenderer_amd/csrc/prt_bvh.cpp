@@ -47,7 +47,7 @@ struct TNode {
     int32_t count = 0;               // > 0 for leaves
 };
 
-constexpr int kMaxBins = 64;
+constexpr int kMaxBins = 128;
 
 // ---------------------------------------------------------- early split clipping
 // A triangle far larger than the scene's typical one (the Cornell walls among config 4's
@@ -155,7 +155,7 @@ inline Box outward_f32(const RefBox& r, const Box& tri_box) {
 struct Builder {
     const float* tv;           // triangle vertices (n_tri x 9)
     int max_leaf;
-    int bins = 32;             // SAH bins per axis (env PRT_SAH_BINS, 2..64)
+    int bins = 32;             // SAH bins per axis (env PRT_SAH_BINS, 2..128; 64 for large scenes)
     double ct = 0.5;           // SAH cost of a node step relative to one triangle test (env PRT_SAH_CT)
     int leaf_min = 2;          // ranges of <= leaf_min triangles always become leaves (env PRT_LEAF_MIN)
     bool sbvh = true;          // spatial splits (env PRT_SBVH=0 turns them off)
@@ -548,6 +548,12 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     if (n_tri < 0 || n_tri >= ((int64_t)1 << 27)) { *err = "triangle count out of range (< 2^27)"; return false; }
     Builder B;
     B.tv = tri_v; B.max_leaf = max_leaf;
+    // scenes of >= 2^14 triangles (never LDS-resident) build finer: 64 SAH bins, early split clipping
+    // above 128 x the mean box area, treelet restructuring (config 4: node visits 144.3 -> 138.1 per
+    // sample against 32 bins / 64 x / no treelets, profiles/r05/treelet/); the small LDS scenes keep
+    // the round-4 tree (the restructured Cornell tree collapses to a BVH4 that visits more nodes)
+    const bool large = n_tri >= (1 << 14);
+    if (large) B.bins = 64;
     if (const char* e = std::getenv("PRT_SAH_BINS")) B.bins = std::max(2, std::min(kMaxBins, std::atoi(e)));
     if (const char* e = std::getenv("PRT_SBVH")) B.sbvh = std::atoi(e) != 0;
     if (const char* e = std::getenv("PRT_SBVH_ALPHA")) B.alpha = std::max(0.0, std::atof(e));
@@ -574,7 +580,7 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
     mean_area /= (double)std::max<int64_t>(n_tri, 1);
     // references: one per triangle, several (early split clipping) for triangles whose box
     // area exceeds esc_beta x the mean (env PRT_ESC_BETA, 0 = off; at most 2 n_tri + 4096)
-    double esc_beta = 64.0;
+    double esc_beta = large ? 128.0 : 64.0;
     if (const char* e = std::getenv("PRT_ESC_BETA")) esc_beta = std::max(0.0, std::atof(e));
     std::vector<int32_t>& ref_tri = B.ref_tri;
     ref_tri.reserve((size_t)n_tri);
@@ -627,11 +633,11 @@ bool build_bvh(const float* tri_v, int64_t n_tri, int max_leaf, BvhHost* out, st
         B.nodes.reserve((size_t)(2 * n_ref0 / std::max(1, max_leaf / 2) + 8));
         if (scene.valid()) B.min_overlap = B.alpha * scene.area();
         root = B.build(all, 0);
-        // treelet restructuring passes (env PRT_TREELET, 0 = off): on by default for scenes of >= 2^14
-        // triangles (config 4: BVH2 SAH -3 %, node visits -2.1 %, 157.5 -> 154.6 ms per launch); the
-        // small LDS-resident scenes keep the plain tree, whose BVH4 collapse visits fewer nodes there
+        // treelet restructuring passes (env PRT_TREELET, 0 = off): on by default for large scenes
+        // (config 4: BVH2 SAH -3 %, node visits -2.1 %, 157.5 -> 154.6 ms per launch); the small
+        // LDS-resident scenes keep the plain tree, whose BVH4 collapse visits fewer nodes there
         // (Cornell: 22.7 vs 26.3 node visits per sample with the restructured tree, profiles/r05/treelet/)
-        int passes = n_tri >= (1 << 14) ? 3 : 0;
+        int passes = large ? 3 : 0;
         if (const char* e = std::getenv("PRT_TREELET")) passes = std::max(0, std::min(8, std::atoi(e)));
         if (passes > 0 && B.nodes[root].count == 0) {
             restructure_treelets(B.nodes, root, B.ct, passes);
