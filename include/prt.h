@@ -40,8 +40,8 @@ extern "C" {
  * straight into a padded per-frame buffer; PRT_FLAG_NO_PRIMARY_KERNEL, accepted by ABI 2, is
  * rejected with PRT_ERR_UNSUP; prt_scatter_frames and prt_camera_rays added; variant ids 9 / 10 (the pooled kernel's
  * fused schedule, 7 / 6 waves per SIMD: extension traversals also answer the pooled shadow rays)
- * and 11 / 12 (the pooled kernel with packed leaf trips) added, ids above 12 rejected with
- * PRT_ERR_ARG. */
+ * 11 / 12 (the pooled kernel with packed leaf trips) and 13 / 14 (the pooled kernel without its
+ * block barrier) added, ids above 14 rejected with PRT_ERR_ARG. */
 #define PRT_ABI_VERSION 3
 
 #define PRT_OK 0
@@ -71,7 +71,8 @@ extern "C" {
  * SIMD), 2 the same without an occupancy target, 3 global scene (quantised nodes, spill
  * stack), 4 / 5 the MIS estimator on an LDS / global scene, 6 the LDS-resident scene built
  * for >= 6 waves per SIMD, 7 / 8 the LDS-resident block-pooled shadow kernel for >= 7 / >= 6
- * waves per SIMD, 9 / 10 its fused schedule, 11 / 12 it with packed leaf trips).  Variants of one
+ * waves per SIMD, 9 / 10 its fused schedule, 11 / 12 it with packed leaf trips, 13 / 14 it without
+ * the block barrier).  Variants of one
  * estimator produce
  * bit-identical images; the selector exists for A/B runs and tests. */
 #define PRT_FLAG_VARIANT_SHIFT 8

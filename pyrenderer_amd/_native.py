@@ -31,10 +31,13 @@ VAR_LDS_FUSED = 9     # trace_kernel_pool's FUSED schedule: extension traversals
 VAR_LDS_FUSED6 = 10   # VAR_LDS_FUSED built for >= 6 waves/SIMD
 VAR_LDS_PACK = 11     # trace_kernel_pool, two-phase, packed leaf trips (traverse_pk)
 VAR_LDS_PACK6 = 12    # VAR_LDS_PACK built for >= 6 waves/SIMD
+VAR_LDS_SPLIT = 13    # trace_kernel_pool, two-phase without the block barrier (split arrival)
+VAR_LDS_SPLIT6 = 14   # VAR_LDS_SPLIT built for >= 6 waves/SIMD
 VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_FUSED,
-                 VAR_LDS_FUSED6, VAR_LDS_PACK, VAR_LDS_PACK6)
-VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_FUSED, VAR_LDS_FUSED6, VAR_LDS_PACK, VAR_LDS_PACK6)
-VAR_LAST = 12
+                 VAR_LDS_FUSED6, VAR_LDS_PACK, VAR_LDS_PACK6, VAR_LDS_SPLIT, VAR_LDS_SPLIT6)
+VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_FUSED, VAR_LDS_FUSED6, VAR_LDS_PACK, VAR_LDS_PACK6, VAR_LDS_SPLIT,
+            VAR_LDS_SPLIT6)
+VAR_LAST = 14
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 

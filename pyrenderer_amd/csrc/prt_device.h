@@ -1699,11 +1699,22 @@ constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 
 // C5): without that code the kernel's loop keeps 17 fewer uniform values in spilled SGPRs and is a
 // third shorter
 // PK (round 5, variants 11 / 12): the two-phase schedule with packed leaf trips (traverse_pk, PK held
-// leaves per lane) in the extension and the shadow traversals
-template <bool STATS, int WPE, bool PLAIN, bool FUSED, int PK = 0>
+// leaves per lane) in the extension and the shadow traversals.
+// SPLIT (round 5, variants 13 / 14): the two-phase schedule without the block barrier.  A wave that
+// has enqueued iteration k's shadow rays counts itself in arrive(k) and goes on; the block's S(k)
+// chunks are claimed by waves that find arrive(k) == 4 at the top of their next iteration, and by
+// waves waiting for S(k)'s answers (helping while they wait).  Before it resolves answers at
+// iteration k + 1, every wave waits until all four arrived at k (so no wave runs more than one
+// iteration ahead: queue buffers, pool slots and the control words of three iterations stay safe by
+// the same argument as the barrier's), and a wave with pending shadow rays until S(k) is answered.
+// Waves whose lanes are done and whose refill is exhausted count themselves as ghosts; the block
+// ends when a wave that is a ghost sees four ghosts before it arrives.
+template <bool STATS, int WPE, bool PLAIN, bool FUSED, int PK = 0, bool SPLIT = false>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel_pool(TraceParams P) {
     static_assert(!(FUSED && PK), "one schedule");
+    static_assert(!(SPLIT && (FUSED || PK)), "one schedule");
+    constexpr int ctl_f4 = SPLIT ? kCtlF4 + 1 : kCtlF4;   // SPLIT: word 12 counts the ghost waves
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1713,8 +1724,8 @@ void trace_kernel_pool(TraceParams P) {
     float* pool = reinterpret_cast<float*>(smem + stack_f4);   // [7][256]
     uint8_t* queue = reinterpret_cast<uint8_t*>(smem + stack_f4 + kPoolF4);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + stack_f4 + kPoolF4 + kQueueF4);
-    int8_t* wb = reinterpret_cast<int8_t*>(smem + stack_f4 + kPoolF4 + kQueueF4 + kCtlF4) + (tid & ~63);
-    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + kCtlF4 + (PK ? kPkF4 : 0);
+    int8_t* wb = reinterpret_cast<int8_t*>(smem + stack_f4 + kPoolF4 + kQueueF4 + ctl_f4) + (tid & ~63);
+    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + ctl_f4 + (PK ? kPkF4 : 0);
     const int n_node4 = P.n_node_f4 / 8;
     float4* st4 = sn + 56 * n_node4;
     float4* slv = st4 + P.n_tri_f4;
@@ -1725,7 +1736,7 @@ void trace_kernel_pool(TraceParams P) {
     for (int i = tid; i < 4 * P.n_lt; i += kBlock) slv[i] = P.light_v[i];
     for (int i = tid; i <= P.n_light; i += kBlock) slo[i] = P.light_off[i];
     for (int i = tid; i < 2 * P.n_mat; i += kBlock) smt[i] = reinterpret_cast<const float4*>(P.mats)[i];
-    if (tid < 12) ctl[tid] = 0u;
+    if (tid < 4 * ctl_f4) ctl[tid] = 0u;
     __syncthreads();
     const float4* g_nodes = sn;
     const float4* g_tris = st4;
@@ -1770,6 +1781,9 @@ void trace_kernel_pool(TraceParams P) {
     uint32_t qpar = 0, qpar_prev = 0;
     // FUSED: rays in the previous iteration's queue, answered in this iteration's traversal
     uint32_t nq_prev = 0;
+    // SPLIT: iterations done, this wave counted as a ghost
+    uint32_t it_k = 0;
+    bool ghost = false;
 #ifdef PRT_POOL_CLOCKS
     // diagnostic build (tools/pool_clocks.py): wave-level cycles in E, at barrier 1, in S, at barrier 2
     uint64_t ck[6] = {0, 0, 0, 0, 0, 0};
@@ -1844,9 +1858,59 @@ void trace_kernel_pool(TraceParams P) {
             }
         if (item == -2) item = -1;
     };
+    // SPLIT: one 64-ray chunk of the queue of the iteration in control slot s_slot / queue buffer s_qpar
+    auto run_chunk = [&](uint32_t s_slot, uint32_t s_qpar, uint32_t n_q, uint32_t chunk) {
+        __builtin_amdgcn_s_setprio(PRT_POOL_S_PRIO);
+        const uint32_t e0 = chunk * 64u, e1 = min(n_q, e0 + 64u);
+        const uint32_t e = e0 + (uint32_t)lane;
+        if (STATS && lane == 0) { n_s++; lanes_s += e1 - e0; }
+        if (e < e1) {
+            const int owner = queue[s_qpar * kBlock + e];
+            const V3 so = v3(pool[0 * kBlock + owner], pool[1 * kBlock + owner], pool[2 * kBlock + owner]);
+            const V3 sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
+            const float stm = pool[6 * kBlock + owner];
+            int hid = -1;
+            float ht = 0.0f;
+            if (STATS) cn.q0 = cn.nodes;
+            bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
+                g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
+                exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+            if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
+            if (!PLAIN && P.n_sph > 0 && !hit) {
+                for (int k = 0; k < P.n_sph; ++k) {
+                    float root;
+                    if (sphere_hit(P.sph[k], so, sd, kTMin, stm, root)) { hit = true; break; }
+                }
+            }
+            pool[6 * kBlock + owner] = hit ? __int_as_float(0x7FC00000) : 0.0f;
+        }
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&ctl[9 + s_slot], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto ld_acq = [&](int w) { return __hip_atomic_load(&ctl[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto ld_rlx = [&](int w) { return __hip_atomic_load(&ctl[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    // SPLIT: claim one unclaimed chunk of slot s_slot's queue once all four waves arrived there;
+    // false when there is none to claim
+    auto claim_run = [&](uint32_t s_slot, uint32_t s_qpar) -> bool {
+        if (ld_acq(3 + (int)s_slot) < 4u) return false;
+        const uint32_t n_q = ld_rlx((int)s_slot);
+        const uint32_t nch = (n_q + 63u) >> 6;
+        if (ld_rlx(6 + (int)s_slot) >= nch) return false;
+        uint32_t ch = 0;
+        if (lane == 0) ch = atomicAdd(&ctl[6 + s_slot], 1u);
+        ch = __builtin_amdgcn_readfirstlane(ch);
+        if (ch >= nch) return false;
+        run_chunk(s_slot, s_qpar, n_q, ch);
+        return true;
+    };
     while (true) {
         // ------------------------------------------------------------------ E phase
         refill();
+        if constexpr (SPLIT) {
+            // the previous iteration's shadow rays: one chunk, if all waves have arrived there
+            if (it_k > 0) (void)claim_run(slot_prev, qpar_prev);
+        }
         PRT_CLOCK(4);
         if (STATS && item >= 0) book(12);
         // (a) extension traversal: every busy lane except one whose pending shadow ray ends its path
@@ -2047,15 +2111,34 @@ void trace_kernel_pool(TraceParams P) {
         // (b) the previous S phase's answers (its waves ran it beside this wave's traversal; FUSED: the
         // block's traversals of this iteration): a wave with a pending shadow ray waits until every
         // chunk (FUSED: every ray) of the previous queue has been answered
-        if (__ballot(my_sh) != 0) {
+        if (SPLIT ? it_k > 0 : __ballot(my_sh) != 0) {
             // bounded: a wait that never ends (a logic error) raises the watchdog flag instead of
             // hanging the device: 2^20 sleeps of 64 clocks ~ 30 ms, against a worst case of ~0.1 ms for
             // the answers (an LDS scene is <= 24 KiB: a query visits each of its <= ~100 nodes and
             // <= ~500 triangles at most once, ~10^5 cycles even in a STATS build).  A lane whose answer
             // did not arrive ends with NaN radiance (counted by STATS' non-finite samples), so a tripped
             // wait cannot pass for a valid image even before prt_check_faults reports it.
-            const uint32_t need = FUSED ? nq_prev : nch_prev;
             bool late = false;
+            if constexpr (SPLIT) {
+                // every wave: until all four arrived at the previous iteration; a wave with pending
+                // shadow rays: until every chunk of that queue is answered, answering chunks itself
+                const bool need_done = __ballot(my_sh) != 0;
+                for (uint32_t spin = 0;; ++spin) {
+                    if (ld_acq(3 + (int)slot_prev) >= 4u) {
+                        if (!need_done) break;
+                        const uint32_t nch = (ld_rlx((int)slot_prev) + 63u) >> 6;
+                        if (ld_acq(9 + (int)slot_prev) >= nch) break;
+                        if (claim_run(slot_prev, qpar_prev)) continue;
+                    }
+                    if (spin >= (1u << 20)) {
+                        if (lane == 0) atomicOr(P.fault, 2);
+                        late = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            } else {
+            const uint32_t need = FUSED ? nq_prev : nch_prev;
             for (uint32_t spin = 0;
                  need && __hip_atomic_load(&ctl[9 + slot_prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need;
                  ++spin) {
@@ -2065,6 +2148,7 @@ void trace_kernel_pool(TraceParams P) {
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
+            }
             }
             if (my_sh) {
                 if (STATS) book(14);
@@ -2227,12 +2311,34 @@ void trace_kernel_pool(TraceParams P) {
                 if (my_sh) queue[qpar * kBlock + base + rank] = (uint8_t)tid;
             }
             // a wave with busy lanes or unclaimed work keeps the block looping
-            if ((__ballot(item >= 0) != 0 || !exhausted) && lane == 0) ctl[3 + slot] = 1u;
+            if (!SPLIT && (__ballot(item >= 0) != 0 || !exhausted) && lane == 0) ctl[3 + slot] = 1u;
             // the next iteration's words, last used two iterations ago (every wave has read them since)
             if (tid == 0) {
                 const uint32_t ns = slot == 2 ? 0u : slot + 1u;
                 ctl[ns] = 0u; ctl[3 + ns] = 0u; ctl[6 + ns] = 0u; ctl[9 + ns] = 0u;
             }
+        }
+        if constexpr (SPLIT) {
+            // no barrier: count this wave as arrived (after its queue entries, pool slots and the reset
+            // above); a wave with no work left and none to come counts as a ghost once, and the block
+            // ends once a ghost sees all four waves as ghosts before arriving (every wave still waiting
+            // on this iteration has then arrived, and reads four ghosts at its next arrival at the latest)
+            if (!ghost && exhausted && __ballot(item >= 0) == 0) {
+                ghost = true;
+                if (lane == 0) atomicAdd(&ctl[12], 1u);
+            }
+            const bool leave = ghost && ld_acq(12) >= 4u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_fetch_add(&ctl[3 + slot], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            ++it_k;
+            slot_prev = slot;
+            slot = slot == 2 ? 0u : slot + 1u;
+            qpar_prev = qpar;
+            qpar ^= 1u;
+            o = v3(pool[0 * kBlock + tid], pool[1 * kBlock + tid], pool[2 * kBlock + tid]);
+            d = wi;
+            if (leave) break;
+            continue;
         }
         PRT_CLOCK(0);
         __syncthreads();
@@ -2378,10 +2484,14 @@ void trace_kernel_pool(TraceParams P) {
     X(kVarLdsFused, 1536, true, 7)            \
     X(kVarLdsFused6, 1536, true, 6)           \
     X(kVarLdsPack, 2560, true, 7)             \
-    X(kVarLdsPack6, 2560, true, 6)
+    X(kVarLdsPack6, 2560, true, 6)            \
+    X(kVarLdsSplit, 4608, true, 7)            \
+    X(kVarLdsSplit6, 4608, true, 6)
 
-// the pool kernel's schedule of a variant's bits: 1024 FUSED, 2048 packed leaf trips
-constexpr int pool_sched(int bits) { return (bits & 1024) ? kPoolFused : (bits & 2048) ? kPoolPacked : kPoolTwoPhase; }
+// the pool kernel's schedule of a variant's bits: 1024 FUSED, 2048 packed leaf trips, 4096 split arrival
+constexpr int pool_sched(int bits) {
+    return (bits & 1024) ? kPoolFused : (bits & 2048) ? kPoolPacked : (bits & 4096) ? kPoolSplit : kPoolTwoPhase;
+}
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>

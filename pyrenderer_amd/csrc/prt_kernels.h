@@ -84,12 +84,16 @@ constexpr int kVarLdsFused6 = 10;  // kVarLdsFused built for >= 6 waves/SIMD
 constexpr int kVarLdsPack = 11;    // trace_kernel_pool, two-phase, packed leaf trips (round 5): the triangle
                                    // tests of all leaves the wave's lanes hold run 64 to a trip (traverse_pk)
 constexpr int kVarLdsPack6 = 12;   // kVarLdsPack built for >= 6 waves/SIMD
+constexpr int kVarLdsSplit = 13;   // trace_kernel_pool, two-phase without the block barrier (round 5): waves
+                                   // arrive per iteration and answer the shadow chunks they wait for
+constexpr int kVarLdsSplit6 = 14;  // kVarLdsSplit built for >= 6 waves/SIMD
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 12;
+constexpr int kVarLast = 14;
 // trace_kernel_pool schedules
-constexpr int kPoolTwoPhase = 0, kPoolFused = 1, kPoolPacked = 2;
+constexpr int kPoolTwoPhase = 0, kPoolFused = 1, kPoolPacked = 2, kPoolSplit = 3;
 bool variant_pool(int var);
 bool variant_pack(int var);
+bool variant_split(int var);
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
