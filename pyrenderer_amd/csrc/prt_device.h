@@ -1533,6 +1533,14 @@ __device__ __forceinline__ bool traverse_pk(const float4* __restrict__ nodes, co
                                             uint32_t guard_lim) {
     static_assert(NP >= 1 && NP <= 3, "held leaves");
     const int lane = (int)__lane_id();
+    // the pair hand-off (DPP scan, ds_bpermute) assumes every lane of the wave is here: a call from
+    // divergent code is a logic error, reported as watchdog flag 4 (the queries then miss)
+    if (__ballot(true) != ~0ull) {
+        if (fault && lane == __builtin_amdgcn_readfirstlane(lane)) atomicOr(fault, 4);
+        hit_id = -1;
+        hit_t = tmax;
+        return false;
+    }
     const V3 inv = ray_inv(d);
     const V3 oi = o * inv;
     const int sx = 7 * ((__float_as_int(inv.x) < 0 ? 1 : 0) | (__float_as_int(inv.y) < 0 ? 2 : 0) |
@@ -2131,7 +2139,9 @@ void trace_kernel_pool(TraceParams P) {
                         if (claim_run(slot_prev, qpar_prev)) continue;
                     }
                     if (spin >= (1u << 20)) {
-                        if (lane == 0) atomicOr(P.fault, 2);
+                        // a wave that never arrives (a logic error): flag it and let the block end
+                        // without the ghost count (bit 8 of word 12)
+                        if (lane == 0) { atomicOr(P.fault, 2); atomicOr(&ctl[12], 0x100u); }
                         late = true;
                         break;
                     }
@@ -2327,7 +2337,8 @@ void trace_kernel_pool(TraceParams P) {
                 ghost = true;
                 if (lane == 0) atomicAdd(&ctl[12], 1u);
             }
-            const bool leave = ghost && ld_acq(12) >= 4u;
+            const uint32_t gw = ld_acq(12);
+            const bool leave = ghost && ((gw & 0xFFu) >= 4u || (gw & 0x100u) != 0u);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (lane == 0) __hip_atomic_fetch_add(&ctl[3 + slot], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             ++it_k;
