@@ -133,6 +133,35 @@ def test_bvh_build_covers_every_triangle_with_conservative_boxes(sbvh, treelet, 
         assert tri[i] in _traverse_py(nodes, tris, order, ro[i].astype(np.float64), rd[i].astype(np.float64), 1e-5, 1e5)
 
 
+@pytest.mark.parametrize("treelet", ["0", "3"])
+def test_bvh_depth_is_the_exported_trees_depth(treelet, monkeypatch):
+    """The depth prt_bvh_info reports (it sizes the traversal stacks) is the exported BVH2's, also after
+    treelet restructuring has moved inner nodes (prt_bvh.cpp tree_depth); every inner node is reached
+    once from the root."""
+    import struct
+    from pyrenderer_amd import _native as N
+    monkeypatch.setenv("PRT_TREELET", treelet)
+    rng = np.random.default_rng(11)
+    n = 5000
+    c = rng.uniform(-5, 5, (n, 1, 3)) * rng.uniform(0.2, 1.0, (n, 1, 3)) ** 2
+    tv = (c + rng.normal(0, 0.05, (n, 3, 3))).astype(np.float32).reshape(n, 9)
+    b = N.Bvh(tv, max_leaf=4)
+    nodes, _, _ = b.export()
+    seen = np.zeros(len(nodes), np.int32)
+    deepest, stack = 0, [(0, 0)]
+    while stack:
+        i, d = stack.pop()
+        seen[i] += 1
+        for side in (0, 1):
+            r = struct.unpack("<i", struct.pack("<f", nodes[i][12 + side]))[0]
+            if r >= 0:
+                stack.append((r, d + 1))
+            else:
+                deepest = max(deepest, d + 1)
+    assert (seen == 1).all()
+    assert b.depth == deepest
+
+
 def test_bvh_degenerate_inputs():
     from pyrenderer_amd import _native as N
     b = N.Bvh(np.zeros((0, 9), np.float32))
