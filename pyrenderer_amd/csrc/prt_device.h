@@ -457,13 +457,13 @@ __device__ __forceinline__ bool slab_nf(float nx, float fx, float ny, float fy, 
     float ay = __builtin_fmaf(ny, inv.y, -oi.y), by = __builtin_fmaf(fy, inv.y, -oi.y);
     float az = __builtin_fmaf(nz, inv.z, -oi.z), bz = __builtin_fmaf(fz, inv.z, -oi.z);
     float tnear = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin));
-    // the reference's 1 + 2 gamma_3 factor on t_far (bvh_taichi.py:179) is off (round 5): the box
-    // padding (1e-6 of the scene's largest coordinate, ~8 ulps) already covers the estimate's few-ulp
-    // error (1/d within 1 ulp, o/d rounded, one fma rounding), so the test stays conservative without
-    // it — 4 VALU per node visit, C2 3.873 vs 3.884, C3 70.75 vs 71.14 ms per launch, images
-    // identical (profiles/r05/gamma/); -D PRT_SLAB_GAMMA=1 restores it
+    // the reference's 1 + 2 gamma_3 factor on t_far (bvh_taichi.py:179).  The box padding (1e-6 of
+    // the scene's largest coordinate, ~8 ulps) alone would keep the test conservative, and dropping the
+    // factor saves 4 VALU per visit (-D PRT_SLAB_GAMMA=0: C2 3.873 vs 3.884, C3 70.75 vs 71.14 ms per
+    // launch, images identical), but the pooled kernel then spills 3 VGPRs and writes 0.14 GB more
+    // per frame to HBM (profiles/r05/gamma/): kept
 #ifndef PRT_SLAB_GAMMA
-#define PRT_SLAB_GAMMA 0
+#define PRT_SLAB_GAMMA 1
 #endif
     float tfar = fminf(fminf(bx, by), fminf(bz, tmax));
     if (PRT_SLAB_GAMMA) tfar *= kGamma;
