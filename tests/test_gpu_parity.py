@@ -247,6 +247,25 @@ def test_specular_scene_matches_oracle(rough, kernel):
     assert same >= 0.999, same
 
 
+def test_pool_variants_identical_on_the_specular_scene():
+    """Every schedule of the pooled kernel's full build (spheres, metal, dielectric: two-phase, fused,
+    packed leaf trips, split arrival; 7 and 6 waves per SIMD) renders the same bits on config 3's
+    materials, and those bits match the oracle as test_specular_scene_matches_oracle requires."""
+    from pyrenderer_amd import _native as N
+    from pyrenderer_amd.device_scene import DeviceScene
+    scene, cam, flat = _specular_scene(0.35)
+    ds = DeviceScene(flat, 0)
+    c = cam.convert_to_taichi_camera().packed()
+    imgs = {v: _gpu_frame(ds, c, 64, 64, 4, 8, seed=6, flags=v << 8) for v in N.VAR_POOL}
+    first = imgs[N.VAR_LDS_POOL]
+    for v, g in imgs.items():
+        assert np.array_equal(g, first), v
+    o = O.OracleScene.from_flat(flat).render(c, 64, 64, 4, 8, seed=6)
+    rmse, same = _compare(first, o, 4)
+    assert rmse < TOL_RMSE, rmse
+    assert same >= 0.999, same
+
+
 def test_specular_boxes_without_spheres_take_the_full_pooled_build():
     """Metal / dielectric boxes but no sphere: the pooled kernel's lean build (TraceParams::plain)
     must not be chosen — it has no specular code — so the image still matches the oracle."""
