@@ -230,6 +230,13 @@ int prt_render_frames_device(void* scene, const float* cam, int W, int H, int tw
  * traversal watchdog tripped in the last render of any stream (and clears the flags,
  * like prt_check_faults). */
 int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
+
+/* Self-test of the kernels' exact-reciprocal fast sequence (prt_device.h rcp_fast_seq: v_rcp_f32, one
+ * refinement, two corrections) against the IEEE division 1.0f / b for every one of the 2^32 floats
+ * on `device`; mismatches8 = mismatches by the class of |b|: 0 zero, 1 denormal, 2 normal < 2^-40,
+ * 3 [2^-40, 2^40] (the range the kernels use the sequence in), 4 (2^40, 2^126], 5 > 2^126 finite,
+ * 6 infinite, 7 NaN (both results NaN count as equal).  ABI 3, round 5. */
+int prt_selftest_rcp(int device, uint64_t* mismatches8);
 /* Failure detection for renders whose result stays on the device (prt_render_tiles_device,
  * the torch.distributed path): synchronises the device, then reports PRT_ERR_INTERNAL if
  * the traversal watchdog tripped in the last render enqueued on any of this scene's

@@ -1131,6 +1131,22 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
     return PRT_OK;
 }
 
+int prt_selftest_rcp(int device, uint64_t* mismatches8) {
+    if (!mismatches8) return fail(PRT_ERR_ARG, "NULL argument");
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return fail(PRT_ERR_HIP, "no such HIP device");
+    DeviceGuard g(device);
+    DevBuf d;
+    HIP_TRY(d.ensure(8 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(d.p, 0, 8 * sizeof(unsigned long long)));
+    HIP_TRY(prt::launch_rcp_selftest((unsigned long long*)d.p, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long h[8];
+    HIP_TRY(hipMemcpy(h, d.p, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 8; ++i) mismatches8[i] = h[i];
+    return PRT_OK;
+}
+
 int prt_check_faults(void* scene) {
     auto* s = (Scene*)scene;
     if (!s) return fail(PRT_ERR_ARG, "NULL argument");

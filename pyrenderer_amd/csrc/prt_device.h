@@ -96,14 +96,16 @@ __device__ __forceinline__ V3 div3_nan_guard(V3 a, float pdf) {
 // 1 / b, correctly rounded: for finite |b| in [2^-40, 2^40] the division expansion (see
 // div3) with numerator 1 is the refined reciprocal plus two quotient corrections
 // (its q = 1 * r is exact); other waves take the plain division.
+// the sequence itself (prt_selftest_rcp compares it with the IEEE division over all 2^32 floats)
+__device__ __forceinline__ float rcp_fast_seq(float b) {
+    float r = __builtin_amdgcn_rcpf(b);
+    r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+    const float q = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+    return __builtin_fmaf(__builtin_fmaf(-b, q, 1.0f), r, q);
+}
 __device__ __forceinline__ float rcp_exact(float b) {
     const float ab = fabsf(b);
-    if (__ballot(!(ab >= 0x1p-40f && ab <= 0x1p40f)) == 0) {
-        float r = __builtin_amdgcn_rcpf(b);
-        r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
-        const float q = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
-        return __builtin_fmaf(__builtin_fmaf(-b, q, 1.0f), r, q);
-    }
+    if (__ballot(!(ab >= 0x1p-40f && ab <= 0x1p40f)) == 0) return rcp_fast_seq(b);
     return 1.0f / b;
 }
 // Correctly rounded sqrt.  hipcc expands sqrtf on gfx950 as: scale x by 2^32 when

@@ -128,6 +128,9 @@ hipError_t launch_scatter_frames(const float* packed, const uint32_t* tile_xy, i
                                  int64_t group_pitch, int n_frames, int64_t src_fpitch, int64_t dst_fpitch, int log_tw,
                                  int log_tpx, int x0, int y0, int w, int h, float* out, hipStream_t stream);
 int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
+// mismatches of the fast reciprocal sequence against 1 / b over all 2^32 floats, by class of |b|
+// (8 counters: zero, denormal, < 2^-40, [2^-40, 2^40], (2^40, 2^126], > 2^126, inf, NaN)
+hipError_t launch_rcp_selftest(unsigned long long* d_out, hipStream_t stream);
 // the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
 // the pooled kernel's lean instantiation (no sphere or specular code) runs when P.plain is set
 // (sched: kPoolTwoPhase; kPoolFused, whose extension traversals also answer the previous iteration's

@@ -325,6 +325,32 @@ hipError_t launch_camera(const TraceParams& P, float4* rays, float4* ray_o, hipS
     return hipGetLastError();
 }
 
+namespace {
+// rcp_fast_seq against the IEEE division 1 / b for every float b (one 2^32 sweep): mismatches counted
+// by the class of |b| (prt_selftest_rcp); both NaN counts as equal
+__global__ void rcp_selftest_kernel(unsigned long long* out) {
+    const uint64_t n = 1ull << 32;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float b = __uint_as_float((uint32_t)i);
+        const float r = rcp_fast_seq(b);
+        const float e = 1.0f / b;
+        const bool same = __float_as_uint(r) == __float_as_uint(e) || (r != r && e != e);
+        if (!same) {
+            const float ab = fabsf(b);
+            const int cat = b == 0.0f ? 0 : (b != b ? 7 : (isinf(b) ? 6 : (ab < 0x1p-126f ? 1 : (ab < 0x1p-40f ? 2 :
+                            (ab <= 0x1p40f ? 3 : (ab <= 0x1p126f ? 4 : 5))))));
+            atomicAdd(out + cat, 1ull);
+        }
+    }
+}
+}  // namespace
+
+hipError_t launch_rcp_selftest(unsigned long long* d_out, hipStream_t stream) {
+    rcp_selftest_kernel<<<4096, 256, 0, stream>>>(d_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_reduce(const float* buf, float* acc, int n_slots, int64_t j0, int64_t n, int64_t spp, int64_t f0,
                          int64_t n_frames, int64_t pitch, bool accumulate, hipStream_t stream) {
     if (n_frames <= 0 || n_frames > 65535 || pitch < 3 * (int64_t)n_slots) return hipErrorInvalidValue;
