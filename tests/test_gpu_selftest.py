@@ -17,4 +17,6 @@ def test_fast_reciprocal_is_the_ieee_division_where_the_kernels_use_it():
     report = dict(zip(CLASSES, mism.tolist()))
     print("fast reciprocal mismatches by class:", report)
     assert report["[2^-40, 2^40]"] == 0, report
-    assert report["zero"] == 0 or True   # 1/0: the kernels mask it (Moller-Trumbore's det != 0 test)
+    # measured on gfx950: exact for every normal |b| <= 2^126, not for zero / denormal / huge / infinite
+    # operands (rcp_exact sends those to the division; a zero det is masked by det != 0 anyway)
+    assert report["normal < 2^-40"] == 0 and report["(2^40, 2^126]"] == 0, report
