@@ -102,6 +102,11 @@ def parse():
                     help="torch.distributed backend for N > 1: nccl (= RCCL over xGMI, the default) or gloo "
                          "(tile sums staged through host memory; rehearses the N > 1 path with several ranks "
                          "on one GPU)")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="take the N > 1 step's collective path even at --gpus 1: a process group of one rank "
+                         "under torch.distributed.run (started by bench.py itself), the device-tensor "
+                         "all_gather_object / all_reduce, the async gather into rank 0's device buffer and the "
+                         "root's scatter from it — the RCCL branch of the 8-GPU run, exercised on one GPU")
     ap.add_argument("--single-frame-steps", type=int, default=5,
                     help="extra timed leg after the main one: this many steps of ONE frame per launch (what a "
                          "caller's one-shot render of one frame costs), reported as `single_frame`; 0 = skip "
@@ -248,9 +253,9 @@ def launch_check(args, env=None):
     does not initialise the device on this image).  Returns None when this process should
     render, else an exit code: a child launcher's, or 2 for a mislaunch.
 
-    * `--gpus N > 1` without a launcher (no WORLD_SIZE): start `torch.distributed.run` with N
-      ranks on this node as a CHILD process (never exec: the parent has not touched the GPU,
-      but the child must own it), forward its output and exit with its code.
+    * `--gpus N > 1` (or `--force-collective`) without a launcher (no WORLD_SIZE): start
+      `torch.distributed.run` with N ranks on this node as a CHILD process (never exec: the parent
+      has not touched the GPU, but the child must own it), forward its output and exit with its code.
     * under a launcher: WORLD_SIZE must equal --gpus, and for --backend nccl (RCCL: one rank per
       device) N must not exceed the visible devices — either mismatch would print a plausible
       line for the wrong N."""
@@ -265,7 +270,7 @@ def launch_check(args, env=None):
               f"{n_dev} visible", file=sys.stderr)
         return 2
     if "WORLD_SIZE" not in env:
-        if args.gpus == 1:
+        if args.gpus == 1 and not getattr(args, "force_collective", False):
             return None
         import subprocess
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
@@ -326,8 +331,11 @@ def main():
     # ranks share devices round-robin
     n_dev = max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local % n_dev if world > 1 else 0)
-    gloo = world > 1 and args.backend == "gloo"
-    if world > 1:
+    # the collective path (process group, gather to rank 0's buffer, the root's scatter): every N > 1
+    # run, and N = 1 with --force-collective (the same code on a world of one rank)
+    coll = world > 1 or args.force_collective
+    gloo = coll and args.backend == "gloo"
+    if coll:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(dev)
         if gloo:
@@ -341,7 +349,7 @@ def main():
     # nccl ranks share a device is refused (exit 2) on every rank alike
     ident = rank_identity(dev, rank, local)
     ranks = [ident]
-    if world > 1:
+    if coll:
         ranks = [None] * world
         dist.all_gather_object(ranks, ident)
         why = check_rank_devices(ranks, args.backend)
@@ -388,7 +396,8 @@ def main():
         # Multi-frame launches already amortise the drain: serial launches.
         n_streams = 1 if F > 1 else (3 if rank_samples < 8e6 else (2 if world > 1 else 1))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
-    shards = [TileShard(W, H, T, rank, world, dev, args.scheme, host_staging=gloo, frames=F) for _ in range(n_streams)]
+    shards = [TileShard(W, H, T, rank, world, dev, args.scheme, host_staging=gloo, frames=F, collective=coll)
+              for _ in range(n_streams)]
     my_tiles = shards[0].tiles
     n_step = [0]
     rflags = args.variant << 8
@@ -412,7 +421,7 @@ def main():
                                     out_pitch=shard.pitch)
         with torch.cuda.stream(stream):
             shard.gather(n_frames=nf)    # RCCL gathers of per-tile radiance sums to rank 0 (ordered after the frames)
-            if world > 1 and rank == 0:
+            if coll and rank == 0:
                 # root: every rank's tiles of the group's frames into the (W, H, 3) device frames
                 # (SURVEY.md §8(e)), one launch, inside the step
                 shard.scatter_frames(ds, stream, nf)
@@ -430,19 +439,19 @@ def main():
     torch.cuda.synchronize(dev)
     st = np.append(ds.last_stats().astype(np.float64), float(ds.diag_stats()[14]))
     cnt = torch.tensor(st, dtype=torch.float64, device=coll_dev)
-    if world > 1:
+    if coll:
         dist.all_reduce(cnt)
     nodes, tris, ext, shadow, nonfinite = cnt.tolist()
 
     # warmup: the W steps, and at least one full group of F frames (its buffers are then allocated)
     run(max(args.warmup, F))
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize(dev)
     timing[0] = True
     t0 = time.perf_counter()
     run(args.steps)
-    if world > 1:
+    if coll:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
@@ -453,31 +462,41 @@ def main():
     t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=coll_dev)
     # every rank's own timed-region wall time (imbalance shows as max / min)
     per_rank = [t[0:1].clone() for _ in range(world)]
-    if world > 1:
+    if coll:
         dist.all_gather(per_rank, t[0:1].clone())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_avg_ms = t.tolist()
     rank_ms = [float(x.item()) * 1e3 / args.steps for x in per_rank]
+    groups_timed = -(-args.steps // F)
+    f_group = -(-args.steps // groups_timed)   # frames of the timed groups (the first ones; equal groups)
+
+    # the accuracy sample comes from the headline's own launches: rank 0 copies frame 0 of
+    # the last timed group (samples 0 .. spp - 1, rendered inside a multi-frame launch, gathered and, at
+    # N > 1 or with --force-collective, scattered from the gather buffer) before any other leg renders
+    timed_frame = None
+    if rank == 0 and not args.no_cpu_baseline:
+        last = shards[(n_step[0] - 1) % n_streams]
+        timed_frame = last.assemble(ds, streams[(n_step[0] - 1) % n_streams])
 
     # what batching buys: the same step with ONE frame per persistent launch, timed the
     # same way (barrier + synchronize on both sides, max over ranks), after the main leg
     single = None
     if F > 1 and args.single_frame_steps > 0:
         steps(1, 0)                                  # warm the single-frame buffers and launch shape
-        if world > 1:
+        if coll:
             dist.barrier()
         torch.cuda.synchronize(dev)
         ds.kernel_timing()
         t1 = time.perf_counter()
         for _ in range(args.single_frame_steps):
             steps(1, N.PRT_FLAG_TIME)
-        if world > 1:
+        if coll:
             dist.barrier()
         torch.cuda.synchronize(dev)
         el1 = time.perf_counter() - t1
         k1_ms, k1_n = ds.kernel_timing()
         t1v = torch.tensor([el1, k1_ms / max(k1_n, 1)], dtype=torch.float64, device=coll_dev)
-        if world > 1:
+        if coll:
             dist.all_reduce(t1v, op=dist.ReduceOp.MAX)
         el1, k1_avg = t1v.tolist()
         ms1 = el1 * 1e3 / args.single_frame_steps
@@ -531,8 +550,7 @@ def main():
         if not args.no_cpu_baseline and world == 1 and args.numpy_seconds > 0:
             cpu_np, np_ids, np_sums = numpy_baseline(flat, cam, args, args.numpy_seconds)
             if np_ids is not None:
-                torch.cuda.synchronize(dev)
-                cmp = l2_vs_cpu(shards[0].assemble(ds), np_ids, np_sums, args)
+                cmp = l2_vs_cpu(timed_frame, np_ids, np_sums, args)
                 cpu_np["l2_vs_gpu"] = {k: cmp[k] for k in ("pixels", "rmse", "max_pixel_l2", "identical_pixels")}
                 # main.py:52's own parallelism (joblib n_jobs=4), on a shorter sample
                 n4, _, _ = numpy_baseline(flat, cam, args, args.numpy_seconds / 2, procs=4)
@@ -543,8 +561,9 @@ def main():
             ids, cpu_sums, dt, cores = cpu_sample(flat, cam, args, args.cpu_seconds if world == 1 else 2.0)
             if world == 1:
                 cpu = cpu_baseline(ids, dt, cores, args)
-            torch.cuda.synchronize(dev)
-            l2 = l2_vs_cpu(shards[0].assemble(ds), ids, cpu_sums, args)
+            l2 = l2_vs_cpu(timed_frame, ids, cpu_sums, args)
+            l2.update({"source": "timed group", "frame": 0, "frames_per_launch": f_group,
+                       "gathered": bool(coll)})
         hbm_measured = round(traffic / kern_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None
         flops_tf = flops_launch / kern_s / 1e12
         # the dominant kernel's name as rocprofv3 reports it (profiles/*/kernel_stats.csv)
@@ -597,7 +616,7 @@ def main():
             "config": {"workload": f"{SCENE_NAMES[args.scene]} {W}x{H}, {args.spp} spp, depth {args.depth}",
                        "baseline_config": args.config, "triangles": int(flat.n_tri), "spheres": int(flat.sph.shape[0]),
                        "global_batch": W * H * args.spp, "parallelism": f"tiles{world}",
-                       "backend": (args.backend if world > 1 else None),
+                       "backend": (args.backend if coll else None), "collective": bool(coll),
                        "tile_scheme": args.scheme, "frames_in_flight": n_streams, "frames_per_launch": -(-args.steps // -(-args.steps // F)),
                        "tile": T, "bvh_depth": ds.bvh_depth, "bvh_nodes": ds.n_nodes, "scene_build_s": round(t_build, 3),
                        "ranks": ranks},
@@ -618,7 +637,7 @@ def main():
             "l2_vs_cpu": l2,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
 
 

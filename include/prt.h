@@ -35,14 +35,15 @@ extern "C" {
  * check prt_abi_version()); prt_scene_info's info8[4] is the BVH4 LDS traversal stack depth (0:
  * BVH4 too deep for the LDS-stack variants); watchdog flags are cleared once reported
  * (prt_check_faults).
- * ABI 3 (this build): prt_render_frames_device (round 4) takes an output pitch between frames
+ * ABI 3 (round 5): prt_render_frames_device (round 4) takes an output pitch between frames
  * (out_pitch, floats; 0 = packed), so a rank whose shard is shorter than its gather slot can render
- * straight into a padded per-frame buffer; PRT_FLAG_NO_PRIMARY_KERNEL, accepted by ABI 2, is
- * rejected with PRT_ERR_UNSUP; prt_scatter_frames and prt_camera_rays added; variant ids 9 / 10 (the pooled kernel's
- * fused schedule, 7 / 6 waves per SIMD: extension traversals also answer the pooled shadow rays)
- * 11 / 12 (the pooled kernel with packed leaf trips) and 13 / 14 (the pooled kernel without its
- * block barrier) added, ids above 14 rejected with PRT_ERR_ARG. */
-#define PRT_ABI_VERSION 3
+ * straight into a padded per-frame buffer; prt_scatter_frames and prt_camera_rays added; variant
+ * ids 9..14 (three experimental schedules of the pooled kernel) added.
+ * ABI 4 (this build, round 6): variant ids 9..14 removed again (none became the default; DESIGN.md
+ * §9), ids above 8 are rejected with PRT_ERR_ARG as in ABI 2; prt_scatter_frames rejects a
+ * group_pitch too short for n_frames frames at src_frame_pitch; prt_camera_rays zero-fills the rows
+ * of slots outside the frame. */
+#define PRT_ABI_VERSION 4
 
 #define PRT_OK 0
 #define PRT_ERR_ARG (-1)     /* invalid argument / shape */
@@ -71,10 +72,8 @@ extern "C" {
  * SIMD), 2 the same without an occupancy target, 3 global scene (quantised nodes, spill
  * stack), 4 / 5 the MIS estimator on an LDS / global scene, 6 the LDS-resident scene built
  * for >= 6 waves per SIMD, 7 / 8 the LDS-resident block-pooled shadow kernel for >= 7 / >= 6
- * waves per SIMD, 9 / 10 its fused schedule, 11 / 12 it with packed leaf trips, 13 / 14 it without
- * the block barrier).  Variants of one
- * estimator produce
- * bit-identical images; the selector exists for A/B runs and tests. */
+ * waves per SIMD).  Variants of one estimator produce bit-identical images; the selector exists
+ * for A/B runs and tests. */
 #define PRT_FLAG_VARIANT_SHIFT 8
 #define PRT_FLAG_VARIANT(v) (((uint32_t)(v) & 0xFFu) << PRT_FLAG_VARIANT_SHIFT)
 
@@ -185,7 +184,8 @@ int prt_scatter_tiles(void* scene, const float* d_packed, const int32_t* tile_id
  * group_tiles tile slots (frame f at + f * src_frame_pitch floats); tile_ids = n_groups * group_tiles
  * host ids (rank-major, -1 = padding).  Frame f goes to d_frames + f * W*H*3 floats ([x][y]).  The
  * launch covers n_groups * group_tiles slots per frame: the per-rank padding of a ragged shard is
- * one tile list, not (world - 1) * n_frames other frames' slots. */
+ * one tile list, not (world - 1) * n_frames other frames' slots.  ABI 4: with n_groups
+ * > 1, group_pitch >= (n_frames - 1) * src_frame_pitch + group_tiles * tw * th * 3, else PRT_ERR_ARG. */
 int prt_scatter_frames(void* scene, const float* d_packed, const int32_t* tile_ids, int n_groups, int group_tiles,
                        int64_t group_pitch, int tw, int th, int W, int H, int n_frames, int64_t src_frame_pitch,
                        float* d_frames, void* stream);
@@ -277,7 +277,8 @@ int prt_trace_rays(void* scene, const float* rays, int64_t n, int depth, uint64_
  * sample)): samples first_sample .. first_sample + spp - 1 of the tile set's pixels, item order
  * [sample][slot] (slot order of prt_render_tiles).  out8 = n x 8 f32: origin.xyz, the RNG state
  * after the camera's draws (u32 bits), direction.xyz, 0.  Parity / inspection entry point (the host
- * gen_ray of PackedCamera is checked against it).  Synchronous. */
+ * gen_ray of PackedCamera is checked against it).  ABI 4: rows of slots whose pixel lies outside
+ * the frame (partial edge tiles) are all zeros.  Synchronous. */
 int prt_camera_rays(void* scene, const float* cam, int W, int H, int tw, int th, const int32_t* tile_ids,
                     int n_tiles, int first_sample, int spp, uint64_t seed, float* out8);
 /* trace-kernel variant chosen for this scene's large launches when flags select none:

@@ -10,7 +10,7 @@ import numpy as np
 
 from .build import LIB
 
-ABI_VERSION = 3        # include/prt.h PRT_ABI_VERSION
+ABI_VERSION = 4        # include/prt.h PRT_ABI_VERSION
 PRT_OK = 0
 PRT_ERR_UNSUP = -5      # feature not supported by this build
 PRT_ERR_INTERNAL = -6   # device-side check failed (traversal watchdog)
@@ -27,17 +27,10 @@ VAR_MIS = (4, 5)      # MIS estimator: LDS scene, global scene
 VAR_LDS6 = 6          # VAR_LDS built for >= 6 waves/SIMD (LDS copies that fit 6 but not 7 blocks per CU)
 VAR_LDS_POOL = 7      # LDS-resident scene, block-pooled shadow queries (trace_kernel_pool)
 VAR_LDS_POOL6 = 8     # VAR_LDS_POOL built for >= 6 waves/SIMD
-VAR_LDS_FUSED = 9     # trace_kernel_pool's FUSED schedule: extension traversals also answer pooled shadow rays
-VAR_LDS_FUSED6 = 10   # VAR_LDS_FUSED built for >= 6 waves/SIMD
-VAR_LDS_PACK = 11     # trace_kernel_pool, two-phase, packed leaf trips (traverse_pk)
-VAR_LDS_PACK6 = 12    # VAR_LDS_PACK built for >= 6 waves/SIMD
-VAR_LDS_SPLIT = 13    # trace_kernel_pool, two-phase without the block barrier (split arrival)
-VAR_LDS_SPLIT6 = 14   # VAR_LDS_SPLIT built for >= 6 waves/SIMD
-VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_FUSED,
-                 VAR_LDS_FUSED6, VAR_LDS_PACK, VAR_LDS_PACK6, VAR_LDS_SPLIT, VAR_LDS_SPLIT6)
-VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6, VAR_LDS_FUSED, VAR_LDS_FUSED6, VAR_LDS_PACK, VAR_LDS_PACK6, VAR_LDS_SPLIT,
-            VAR_LDS_SPLIT6)
-VAR_LAST = 14
+VAR_REFERENCE = (VAR_LDS, VAR_LDS_ANY_OCC, VAR_GLOBAL, VAR_LDS6, VAR_LDS_POOL, VAR_LDS_POOL6)
+VAR_POOL = (VAR_LDS_POOL, VAR_LDS_POOL6)
+# ids 9-14 (round 5's fused / packed-leaf / split-arrival pooled schedules) were removed in round 6
+VAR_LAST = 8
 PRT_HITS_ANY = 0x1
 PRT_HITS_QUANTIZED = 0x2
 

@@ -984,17 +984,30 @@ int prt_camera_rays(void* scene, const float* cam, int W, int H, int tw, int th,
     P.seed_lo = (uint32_t)seed; P.seed_hi = (uint32_t)(seed >> 32);
     P.s0 = first_sample;
     P.j0 = 0;
+    // one frame of spp samples starting at first_sample, as enqueue_render keys it (global_sample
+    // divides by frame_spp)
+    P.frame_spp = (uint32_t)spp;
+    P.frame_stride = 0;
     P.n_items = (uint64_t)n;
     P.cam_clears = 0;
+    // slots outside the frame (partial edge tiles) get no ray from the camera kernel: their rows are
+    // returned as zeros, not as uninitialised device memory
+    HIP_TRY(hipMemsetAsync(d_rays.p, 0, 16 * (size_t)n, s->stream));
+    if (!P.cam_fast) HIP_TRY(hipMemsetAsync(d_org.p, 0, 16 * (size_t)n, s->stream));
     HIP_TRY(prt::launch_camera(P, (float4*)d_rays.p, P.cam_fast ? nullptr : (float4*)d_org.p, s->stream));
     std::vector<float> r((size_t)n * 4), o(P.cam_fast ? 0 : (size_t)n * 4);
     HIP_TRY(hipMemcpyAsync(r.data(), d_rays.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
     if (!P.cam_fast) HIP_TRY(hipMemcpyAsync(o.data(), d_org.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    const int64_t tpx = (int64_t)tw * th;
     for (int64_t i = 0; i < n; ++i) {
         float* q = out8 + 8 * i;
+        // slot -> pixel as the kernels map it (pixel_of): tile-major, then row-major within the tile
+        const int64_t slot = i % n_slots, loc = slot % tpx;
+        const uint32_t xy0 = origins[(size_t)(slot / tpx)];
+        const bool in_frame = (int64_t)(xy0 >> 16) + loc % tw < W && (int64_t)(xy0 & 0xFFFFu) + loc / tw < H;
         for (int k = 0; k < 3; ++k) {
-            q[k] = P.cam_fast ? P.cam_o[k] : o[(size_t)(4 * i + k)];
+            q[k] = !in_frame ? 0.0f : P.cam_fast ? P.cam_o[k] : o[(size_t)(4 * i + k)];
             q[4 + k] = r[(size_t)(4 * i + k)];
         }
         q[3] = r[(size_t)(4 * i + 3)];   // the RNG state after the camera's draws (u32 bits)
@@ -1296,6 +1309,10 @@ int prt_scatter_frames(void* scene, const float* d_packed, const int32_t* tile_i
     if (group_pitch < 0 || src_frame_pitch < 0 || (n_groups > 1 && group_pitch < group_tiles * slot_f) ||
         (n_frames > 1 && src_frame_pitch < group_tiles * slot_f))
         return fail(PRT_ERR_ARG, "group_pitch / src_frame_pitch must hold a group's tiles");
+    // a group holds all n_frames frames of its tiles: frame f of group g must not reach into group g + 1
+    // 
+    if (n_groups > 1 && group_pitch < (int64_t)(n_frames - 1) * src_frame_pitch + group_tiles * slot_f)
+        return fail(PRT_ERR_ARG, "group_pitch must hold n_frames frames of a group at src_frame_pitch");
     if ((int64_t)n_groups * group_tiles >= ((int64_t)1 << 31)) return fail(PRT_ERR_ARG, "too many tiles");
     return scatter_enqueue(scene, d_packed, tile_ids, n_groups * group_tiles, tw, th, W, H, group_tiles, group_pitch,
                            n_frames, src_frame_pitch, d_frames, 3 * (int64_t)W * H, stream);

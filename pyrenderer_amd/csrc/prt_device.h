@@ -607,38 +607,6 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
     else step(stk);
 }
 
-// One inner-node visit over the LDS octant copy (visit_node4 OCT) for a lane whose query kind is
-// its own (trace_kernel_pool FUSED: a wave's lanes run closest-hit extension and any-hit shadow
-// queries side by side).  Closest-hit lanes take the first hit child of the octant's front-to-back
-// order and push the others; any-hit lanes see the children reversed, so they visit back to front
-// (MODE 2's order: a shadow ray ends at the light, where its occluders are likelier).  The kind
-// only permutes the four (ref, hit) pairs: four selects, then the closest-hit step.
-template <bool STATS>
-__device__ __forceinline__ void visit_oct_mixed(const float4* __restrict__ nodes, int& cur, int& sp, LdsStack16 st,
-                                                V3 inv, V3 oi, int sx, float tmin, float best, bool any,
-                                                Counters& cn) {
-    const LdsF4* nd = as_lds(nodes) + (int)(__umul24((uint32_t)cur, 56u) + (uint32_t)sx);
-    const float4 nx = lds4(nd, 0), fx = lds4(nd, 1), ny = lds4(nd, 2), fy = lds4(nd, 3), nz = lds4(nd, 4),
-                 fz = lds4(nd, 5), rf = lds4(nd, 6);
-    if (STATS) { cn.nodes++; cn.it_inner++; }
-    float t0, t1, t2, t3;
-    const bool h0 = slab_nf(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, oi, inv, tmin, best, t0);
-    const bool h1 = slab_nf(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, oi, inv, tmin, best, t1);
-    const bool h2 = slab_nf(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, oi, inv, tmin, best, t2);
-    const bool h3 = slab_nf(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, oi, inv, tmin, best, t3);
-    const int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z), r3 = __float_as_int(rf.w);
-    const bool b0 = any ? h3 : h0, b1 = any ? h2 : h1, b2 = any ? h1 : h2, b3 = any ? h0 : h3;
-    const int a0 = any ? r3 : r0, a1 = any ? r2 : r1, a2 = any ? r1 : r2, a3 = any ? r0 : r3;
-    const bool p3 = b3 & (b0 | b1 | b2), p2 = b2 & (b0 | b1), p1 = b1 & b0;
-    st.put(sp + 1, a3); sp += p3 ? 1 : 0;
-    st.put(sp + 1, a2); sp += p2 ? 1 : 0;
-    st.put(sp + 1, a1); sp += p1 ? 1 : 0;
-    const int tp = st.get(sp);
-    const bool any_hit = b0 | b1 | b2 | b3;
-    cur = b0 ? a0 : (b1 ? a1 : (b2 ? a2 : (b3 ? a3 : tp)));
-    sp -= any_hit ? 0 : 1;
-}
-
 template <bool STATS, int MODE, class S, bool QN = false, bool RES = false, bool OCT = false>
 __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
                                              V3 d, float tmin, float tmax, bool any_lane, S stk, int& hit_id,
@@ -1501,176 +1469,6 @@ __device__ __forceinline__ void copy_octant_nodes(float4* __restrict__ sn, const
     }
 }
 
-// ------------------------------------------------ packed leaf phase (round 5, PRT_PACK variants)
-// A wave's while-while traversal spends most of its triangle-test trips with few lanes busy
-// (lane table, config 2: 0.29): every lane tests its own leaf one triangle per trip, so a trip
-// count is the wave's LONGEST leaf while most lanes hold short ones or none.  traverse_pk tests
-// the (lane, triangle) pairs of all the leaves the wave's lanes hold 64 to a trip instead: pair p
-// goes to lane p mod 64 of trip p / 64, which fetches the owner's ray and bound from the owner's
-// registers (ds_bpermute), tests the triangle, and the owner folds its pairs' results back in —
-// any-hit: one ballot; closest-hit: a (t, id) minimum over the owner's run of lanes.  The result of
-// a query is the lexicographic minimum (t, id) over its triangle hits whatever the order of the
-// tests (any-hit: whether one exists), so images stay bit-identical.
-constexpr int kPkF4 = 4 * 64 / 16;   // LDS: 64 owner bytes per wave
-
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ int bperm(int src_lane, int v) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
-__device__ __forceinline__ float bperm(int src_lane, float v) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
-}
-// inclusive prefix maximum over the wave: DPP row shifts within each 16-lane row, then the row
-// broadcasts of lanes 15 and 31 (lanes a shift reaches from outside keep the identity)
-__device__ __forceinline__ int wave_max_scan(int v) {
-    constexpr int kId = (int)0x80000000;
-    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x111, 0xf, 0xf, false));   // row_shr:1
-    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x112, 0xf, 0xf, false));   // row_shr:2
-    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x114, 0xf, 0xf, false));   // row_shr:4
-    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x118, 0xf, 0xf, false));   // row_shr:8
-    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
-    v = max(v, __builtin_amdgcn_update_dpp(kId, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
-    return v;
-}
-
-// While-while traversal of the LDS octant BVH4 with packed leaf trips.  Called by ALL 64 lanes of
-// the wave (act: this lane has a query); NP: leaves a lane may hold (postponed) before it stops
-// descending — the leaf phase tests all of them in one round.  wb: the wave's 64 owner bytes.
-// Leaf references of an LDS scene are 16-bit (first < 4096), so two held leaves share a word.
-template <bool STATS, bool ANY, int NP>
-__device__ __forceinline__ bool traverse_pk(const float4* __restrict__ nodes, const float4* __restrict__ tris, V3 o,
-                                            V3 d, float tmax, bool act, LdsStack16 stk, int8_t* wb, int& hit_id,
-                                            float& hit_t, Counters& cn, int* fault, int lb, int le,
-                                            uint32_t guard_lim) {
-    static_assert(NP >= 1 && NP <= 3, "held leaves");
-    const int lane = (int)__lane_id();
-    // the pair hand-off (DPP scan, ds_bpermute) assumes every lane of the wave is here: a call from
-    // divergent code is a logic error, reported as watchdog flag 4 (the queries then miss)
-    if (__ballot(true) != ~0ull) {
-        if (fault && lane == __builtin_amdgcn_readfirstlane(lane)) atomicOr(fault, 4);
-        hit_id = -1;
-        hit_t = tmax;
-        return false;
-    }
-    const V3 inv = ray_inv(d);
-    const V3 oi = o * inv;
-    const int sx = 7 * ((__float_as_int(inv.x) < 0 ? 1 : 0) | (__float_as_int(inv.y) < 0 ? 2 : 0) |
-                        (__float_as_int(inv.z) < 0 ? 4 : 0));
-    stk.put(0, LdsStack16::kSent);
-    int cur = act ? root_for<LdsStack16>(tmax) : LdsStack16::kSent;
-    int sp = 0;
-    float best = tmax;
-    int best_id = -1;
-    bool found = false;
-    // held leaves (first << 3 | count - 1): h01 = leaf 0 | leaf 1 << 16, h2 = leaf 2; nh of them
-    uint32_t h01 = 0, h2 = 0;
-    int nh = 0;
-    auto hold = [&]() {
-        if (cur < 0 && nh == 0) { h01 = (uint32_t)(-cur - 1); nh = 1; cur = stk.get(sp); --sp; }
-        if (NP >= 2 && cur < 0 && nh == 1) { h01 |= (uint32_t)(-cur - 1) << 16; nh = 2; cur = stk.get(sp); --sp; }
-        if (NP >= 3 && cur < 0 && nh == 2) { h2 = (uint32_t)(-cur - 1); nh = 3; cur = stk.get(sp); --sp; }
-    };
-    uint32_t guard = 0;
-    while (true) {
-        // inner phase: descend until at most lb of the descending lanes hold no leaf
-        while (cur >= 0 && cur != LdsStack16::kSent && nh < NP) {
-            visit_node4<STATS, ANY ? 2 : 1, LdsStack16, false, true>(nodes, cur, sp, stk, inv, oi, sx, 0, 0, kTMin,
-                                                                    best, cn);
-            if (STATS) {
-                wave_tick(cn.wi, cn.li);
-                cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
-            }
-            hold();
-            if (__popcll(__ballot(nh == 0)) <= (uint32_t)lb) break;
-        }
-        // leaf rounds (wave-uniform): every held leaf of every lane, 64 pairs per trip
-        while (__ballot(nh > 0) != 0) {
-            const uint32_t v0 = h01 & 0xFFFFu, v1 = h01 >> 16;
-            const int c = (nh > 0 ? (int)(v0 & 7u) + 1 : 0) + (nh > 1 ? (int)(v1 & 7u) + 1 : 0) +
-                          (nh > 2 ? (int)(h2 & 7u) + 1 : 0);   // pairs of this lane, <= 8 NP
-            // exclusive prefix of c over the lanes and the round's total, by bit planes
-            uint32_t pre = 0, total = 0;
-            int steps = 0;   // reduction steps covering the longest run (< 2^steps)
-#pragma unroll
-            for (int b = 0; b < 5; ++b) {
-                const uint64_t m = __ballot((c >> b) & 1);
-                pre += lane_rank(m) << b;
-                total += (uint32_t)__popcll(m) << b;
-                steps = m ? b + 1 : steps;
-            }
-            int carry = -1;
-            for (uint32_t base = 0; base < total; base += 64u) {
-                // owner of pair base + lane: owners mark where their run starts, then a prefix max
-                // (owners ascend with the pair index) fills the runs
-                wb[lane] = (int8_t)-1;
-                if (c > 0 && pre >= base && pre < base + 64u) wb[pre - base] = (int8_t)lane;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                const int owner = wave_max_scan(max((int)wb[lane], carry));
-                carry = __builtin_amdgcn_readlane(owner, 63);
-                const bool valid = base + (uint32_t)lane < total;
-                const V3 qo = v3(bperm(owner, o.x), bperm(owner, o.y), bperm(owner, o.z));
-                const V3 qd = v3(bperm(owner, d.x), bperm(owner, d.y), bperm(owner, d.z));
-                const float ob = bperm(owner, best);
-                const int obid = ANY ? -1 : bperm(owner, best_id);
-                const int opre = bperm(owner, (int)pre), oc = bperm(owner, c);
-                const uint32_t oh01 = (uint32_t)bperm(owner, (int)h01);
-                const uint32_t oh2 = NP >= 3 ? (uint32_t)bperm(owner, (int)h2) : 0u;
-                const int k = (int)(base + (uint32_t)lane) - opre;   // pair k of the owner's run
-                const uint32_t ov0 = oh01 & 0xFFFFu, ov1 = oh01 >> 16;
-                const int oc0 = (int)(ov0 & 7u) + 1, oc1 = (int)(ov1 & 7u) + 1;
-                int ti = k < oc0 ? (int)(ov0 >> 3) + k
-                         : (NP < 3 || k < oc0 + oc1) ? (int)(ov1 >> 3) + (k - oc0)
-                                                     : (int)(oh2 >> 3) + (k - oc0 - oc1);
-                ti = valid ? ti : 0;
-                const LdsF4* tp = as_lds(tris) + (int)__umul24((uint32_t)ti, 3u);
-                const float4 q0 = lds4(tp, 0), q1 = lds4(tp, 1), q2 = lds4(tp, 2);
-                const int id = __float_as_int(q0.w);
-                float t;
-                const bool h = mt_u(xyz(q0), xyz(q1), xyz(q2), qo, qd, kTMin, ob, id, obid, ANY, t) & valid;
-                if (STATS) {
-                    cn.tris += valid ? 1u : 0u;
-                    const uint64_t vm = __ballot(valid);
-                    if (lane == 0) { cn.wl += 1u; cn.ll += (uint32_t)__popcll(vm); cn.it_leaf++; }
-                }
-                // this lane's own run within the trip: lanes [lo, hi)
-                const int lo = max((int)pre - (int)base, 0), hi = min((int)(pre + (uint32_t)c) - (int)base, 64);
-                const bool mine = c > 0 && lo < hi;
-                if (ANY) {
-                    const uint64_t hm = __ballot(h);
-                    const uint64_t span = (hi - lo >= 64) ? ~0ull : ((1ull << (hi - lo)) - 1ull);
-                    if (mine && ((hm >> lo) & span) != 0) found = true;
-                } else {
-                    // (t, id) minimum over the owner's run, toward its first lane: misses are ~0
-                    uint32_t kt = h ? __float_as_uint(t) : 0xFFFFFFFFu, ki = h ? (uint32_t)id : 0xFFFFFFFFu;
-                    const int send = min(opre + oc - (int)base, 64);   // end of the run this lane is in
-                    for (int s = 1, j = 0; j < steps; s <<= 1, ++j) {
-                        const uint32_t at = (uint32_t)bperm(lane + s, (int)kt), ai = (uint32_t)bperm(lane + s, (int)ki);
-                        const bool take = (lane + s < send) & ((at < kt) | ((at == kt) & (ai < ki)));
-                        kt = take ? at : kt;
-                        ki = take ? ai : ki;
-                    }
-                    const uint32_t rt = (uint32_t)bperm(lo, (int)kt), ri = (uint32_t)bperm(lo, (int)ki);
-                    if (mine && ri != 0xFFFFFFFFu) { best = __uint_as_float(rt); best_id = (int)ri; }
-                }
-            }
-            nh = 0; h01 = 0; h2 = 0;
-            if (ANY && found) cur = LdsStack16::kSent;
-            hold();
-            if (__popcll(__ballot(nh > 0)) <= (uint32_t)le) break;
-        }
-        // watchdog (traverse_ww4's)
-        if (++guard > guard_lim) {
-            if (fault && lane == 0) atomicOr(fault, 1);
-            cur = LdsStack16::kSent;
-            nh = 0;
-        }
-        if (__ballot(cur != LdsStack16::kSent || nh > 0) == 0) break;
-    }
-    hit_id = best_id;
-    hit_t = best;
-    return ANY ? found : best_id >= 0;
-}
-
 // Block-pooled shadow queries (LDS-resident scenes, the reference estimator).
 //
 // trace_kernel's phase-aligned waves alternate an extension iteration (62.5 of 64 lanes query at
@@ -1701,7 +1499,7 @@ __device__ __forceinline__ bool traverse_pk(const float4* __restrict__ nodes, co
 // materials) are read from global memory (L1-resident) to keep seven blocks per CU.
 constexpr int kPoolF4 = 7 * kBlock / 4;        // pool SoA: 7 x 256 f32
 constexpr int kQueueF4 = 2 * kBlock / 16;      // queue: 2 x 256 u8, by iteration parity
-constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 6, variant 9 all)
+constexpr int kCtlF4 = 3;                      // ctl: 12 words
 #ifndef PRT_POOL_S_PRIO
 #define PRT_POOL_S_PRIO 2
 #endif
@@ -1717,23 +1515,10 @@ constexpr int kCtlF4 = 3;                      // ctl: 12 words (variant 7 uses 
 // PLAIN: the lean build for scenes without spheres and metal / dielectric materials (P.plain; C1, C2,
 // C5): without that code the kernel's loop keeps 17 fewer uniform values in spilled SGPRs and is a
 // third shorter
-// PK (round 5, variants 11 / 12): the two-phase schedule with packed leaf trips (traverse_pk, PK held
-// leaves per lane) in the extension and the shadow traversals.
-// SPLIT (round 5, variants 13 / 14): the two-phase schedule without the block barrier.  A wave that
-// has enqueued iteration k's shadow rays counts itself in arrive(k) and goes on; the block's S(k)
-// chunks are claimed by waves that find arrive(k) == 4 at the top of their next iteration, and by
-// waves waiting for S(k)'s answers (helping while they wait).  Before it resolves answers at
-// iteration k + 1, every wave waits until all four arrived at k (so no wave runs more than one
-// iteration ahead: queue buffers, pool slots and the control words of three iterations stay safe by
-// the same argument as the barrier's), and a wave with pending shadow rays until S(k) is answered.
-// Waves whose lanes are done and whose refill is exhausted count themselves as ghosts; the block
-// ends when a wave that is a ghost sees four ghosts before it arrives.
-template <bool STATS, int WPE, bool PLAIN, bool FUSED, int PK = 0, bool SPLIT = false>
+template <bool STATS, int WPE, bool PLAIN>
 __global__ __attribute__((amdgpu_flat_work_group_size(kBlock, kBlock), amdgpu_waves_per_eu(WPE)))
 void trace_kernel_pool(TraceParams P) {
-    static_assert(!(FUSED && PK), "one schedule");
-    static_assert(!(SPLIT && (FUSED || PK)), "one schedule");
-    constexpr int ctl_f4 = SPLIT ? kCtlF4 + 1 : kCtlF4;   // SPLIT: word 12 counts the ghost waves
+    constexpr int ctl_f4 = kCtlF4;
     extern __shared__ float4 smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1743,8 +1528,7 @@ void trace_kernel_pool(TraceParams P) {
     float* pool = reinterpret_cast<float*>(smem + stack_f4);   // [7][256]
     uint8_t* queue = reinterpret_cast<uint8_t*>(smem + stack_f4 + kPoolF4);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + stack_f4 + kPoolF4 + kQueueF4);
-    int8_t* wb = reinterpret_cast<int8_t*>(smem + stack_f4 + kPoolF4 + kQueueF4 + ctl_f4) + (tid & ~63);
-    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + ctl_f4 + (PK ? kPkF4 : 0);
+    float4* sn = smem + stack_f4 + kPoolF4 + kQueueF4 + ctl_f4;
     const int n_node4 = P.n_node_f4 / 8;
     float4* st4 = sn + 56 * n_node4;
     float4* slv = st4 + P.n_tri_f4;
@@ -1795,14 +1579,9 @@ void trace_kernel_pool(TraceParams P) {
     // [9..11], one triple entry per iteration mod 3 (a slot is reset two iterations after its use)
     uint32_t slot = 0, slot_prev = 0, nch_prev = 0;
     // the queue's buffer (2 x 256 entries) alternates with the iteration's parity: entries enqueued in
-    // iteration i are read in i's S phase (FUSED: i + 1's traversal), and the next enqueue into the
+    // iteration i are read in i's S phase, and the next enqueue into the
     // same buffer (iteration i + 2) comes after barrier i + 1, which every reader has passed
-    uint32_t qpar = 0, qpar_prev = 0;
-    // FUSED: rays in the previous iteration's queue, answered in this iteration's traversal
-    uint32_t nq_prev = 0;
-    // SPLIT: iterations done, this wave counted as a ghost
-    uint32_t it_k = 0;
-    bool ghost = false;
+    uint32_t qpar = 0;
 #ifdef PRT_POOL_CLOCKS
     // diagnostic build (tools/pool_clocks.py): wave-level cycles in E, at barrier 1, in S, at barrier 2
     uint64_t ck[6] = {0, 0, 0, 0, 0, 0};
@@ -1877,59 +1656,9 @@ void trace_kernel_pool(TraceParams P) {
             }
         if (item == -2) item = -1;
     };
-    // SPLIT: one 64-ray chunk of the queue of the iteration in control slot s_slot / queue buffer s_qpar
-    auto run_chunk = [&](uint32_t s_slot, uint32_t s_qpar, uint32_t n_q, uint32_t chunk) {
-        __builtin_amdgcn_s_setprio(PRT_POOL_S_PRIO);
-        const uint32_t e0 = chunk * 64u, e1 = min(n_q, e0 + 64u);
-        const uint32_t e = e0 + (uint32_t)lane;
-        if (STATS && lane == 0) { n_s++; lanes_s += e1 - e0; }
-        if (e < e1) {
-            const int owner = queue[s_qpar * kBlock + e];
-            const V3 so = v3(pool[0 * kBlock + owner], pool[1 * kBlock + owner], pool[2 * kBlock + owner]);
-            const V3 sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
-            const float stm = pool[6 * kBlock + owner];
-            int hid = -1;
-            float ht = 0.0f;
-            if (STATS) cn.q0 = cn.nodes;
-            bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
-                g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
-                exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-            if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
-            if (!PLAIN && P.n_sph > 0 && !hit) {
-                for (int k = 0; k < P.n_sph; ++k) {
-                    float root;
-                    if (sphere_hit(P.sph[k], so, sd, kTMin, stm, root)) { hit = true; break; }
-                }
-            }
-            pool[6 * kBlock + owner] = hit ? __int_as_float(0x7FC00000) : 0.0f;
-        }
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_fetch_add(&ctl[9 + s_slot], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    auto ld_acq = [&](int w) { return __hip_atomic_load(&ctl[w], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    auto ld_rlx = [&](int w) { return __hip_atomic_load(&ctl[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-    // SPLIT: claim one unclaimed chunk of slot s_slot's queue once all four waves arrived there;
-    // false when there is none to claim
-    auto claim_run = [&](uint32_t s_slot, uint32_t s_qpar) -> bool {
-        if (ld_acq(3 + (int)s_slot) < 4u) return false;
-        const uint32_t n_q = ld_rlx((int)s_slot);
-        const uint32_t nch = (n_q + 63u) >> 6;
-        if (ld_rlx(6 + (int)s_slot) >= nch) return false;
-        uint32_t ch = 0;
-        if (lane == 0) ch = atomicAdd(&ctl[6 + s_slot], 1u);
-        ch = __builtin_amdgcn_readfirstlane(ch);
-        if (ch >= nch) return false;
-        run_chunk(s_slot, s_qpar, n_q, ch);
-        return true;
-    };
     while (true) {
         // ------------------------------------------------------------------ E phase
         refill();
-        if constexpr (SPLIT) {
-            // the previous iteration's shadow rays: one chunk, if all waves have arrived there
-            if (it_k > 0) (void)claim_run(slot_prev, qpar_prev);
-        }
         PRT_CLOCK(4);
         if (STATS && item >= 0) book(12);
         // (a) extension traversal: every busy lane except one whose pending shadow ray ends its path
@@ -1937,181 +1666,14 @@ void trace_kernel_pool(TraceParams P) {
         int hid = -1;
         float ht = 0.0f;
         bool hit = false;
-        if constexpr (FUSED) {
-            // (a) FUSED: the lane's own extension query and the previous iteration's pooled shadow rays in
-            // ONE while-while loop.  A lane without a query (its extension query done, or none this
-            // iteration) claims the next queued shadow ray at the top of every inner + leaf round (one LDS
-            // atomic per wave) and traverses it any-hit, writing the answer into the owner's t_max word:
-            // the lanes that idled in the tail of the wave's extension traversals (lane table, round 5:
-            // inner visits at 44 %, triangle tests at 29 % of the lanes) run the shadow work, and no
-            // separate S phase follows the barrier.  The wave leaves once no lane holds a query and the
-            // queue has no unclaimed ray.  Answers do not depend on who traverses: images are
-            // bit-identical to the two-phase kernel's.
-            const uint32_t n_sq = nq_prev;
-            bool s_more = n_sq != 0u;   // wave-uniform: the previous queue may still hold unclaimed rays
-            bool e_act = trav, s_act = false, any = false;
-            int s_own = 0, cur = LdsStack16::kSent, leaf = 0, sp = 0, best_id = -1, sx = 0;
-            float best = kTMax;
-            V3 qo = o, qd = d, inv = v3(0, 0, 0), oi = v3(0, 0, 0);
-            auto q_init = [&](float tmax) {
-                inv = ray_inv(qd);
-                oi = qo * inv;
-                sx = 7 * ((__float_as_int(inv.x) < 0 ? 1 : 0) | (__float_as_int(inv.y) < 0 ? 2 : 0) |
-                          (__float_as_int(inv.z) < 0 ? 4 : 0));
-                stk.put(0, LdsStack16::kSent);
-                cur = root_for<LdsStack16>(tmax);
-                leaf = 0; sp = 0; best = tmax; best_id = -1;
-                if (STATS) cn.q0 = cn.nodes;
-            };
-            if (STATS && lane == __builtin_amdgcn_readfirstlane(lane) && __ballot(trav) != 0) n_e++;
-            if (trav) {
-                if (STATS) cn.ext++;
-                q_init(kTMax);
-            }
-            const int lb = exhausted ? 0 : P.leaf_break, le = exhausted ? 0 : P.leaf_exit;
-            uint32_t rounds = 0;
-            while (true) {
-                if (s_more) {
-                    const bool fr = !e_act && !s_act;
-                    const uint64_t m = __ballot(fr);
-                    if (m) {
-                        const uint32_t k = (uint32_t)__popcll(m);
-                        uint32_t base = 0;
-                        if (lane == __builtin_amdgcn_readfirstlane(lane)) base = atomicAdd(&ctl[6 + slot_prev], k);
-                        base = __builtin_amdgcn_readfirstlane(base);
-                        if (base + k >= n_sq) s_more = false;
-                        const uint32_t rank =
-                            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        if (fr && base + rank < n_sq) {
-                            s_own = queue[qpar_prev * kBlock + base + rank];
-                            qo = v3(pool[0 * kBlock + s_own], pool[1 * kBlock + s_own], pool[2 * kBlock + s_own]);
-                            qd = v3(pool[3 * kBlock + s_own], pool[4 * kBlock + s_own], pool[5 * kBlock + s_own]);
-                            any = true;
-                            s_act = true;
-                            q_init(pool[6 * kBlock + s_own]);
-                        }
-                    }
-                }
-                const bool act = e_act || s_act;
-                if (__ballot(act) == 0) break;
-                if (act) {
-                    // one round of traverse_ww4's while-while loop: descend until every descending lane
-                    // holds a leaf, then test leaves until at most `le` lanes still hold one
-                    while (cur >= 0 && cur != LdsStack16::kSent) {
-#ifdef PRT_FUSED_MIXED_ORDER
-                        // any-hit lanes back to front (per-lane selects: +18 VALU per visit, round 5)
-                        visit_oct_mixed<STATS>(g_nodes, cur, sp, stk, inv, oi, sx, kTMin, best, any, cn);
-#else
-                        // every lane front to back: the closest-hit visit without per-lane selects (an
-                        // any-hit query's answer does not depend on the order, only its visit count)
-                        visit_node4<STATS, 1, LdsStack16, false, true>(g_nodes, cur, sp, stk, inv, oi, sx, 0, 0, kTMin,
-                                                                       best, cn);
-#endif
-                        if (STATS) {
-                            wave_tick(cn.wi, cn.li);
-                            cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
-                        }
-                        if (cur < 0 && leaf >= 0) {
-                            leaf = cur;
-                            cur = stk.get(sp);
-                            --sp;
-                        }
-                        if (__popcll(__ballot(leaf >= 0)) <= (uint32_t)lb) break;
-                    }
-                    while (leaf < 0) {
-                        const int v = -leaf - 1;
-                        const int first = v >> 3, cnt = (v & 7) + 1;
-                        for (int k = 0; k < cnt; ++k) {
-                            const LdsF4* tp = as_lds(g_tris) + (int)__umul24((uint32_t)(first + k), 3u);
-                            const float4 q0 = lds4(tp, 0), q1 = lds4(tp, 1), q2 = lds4(tp, 2);
-                            const int id = __float_as_int(q0.w);
-                            float t;
-                            if (STATS) { cn.tris++; wave_tick(cn.wl, cn.ll); }
-                            if (mt_u(xyz(q0), xyz(q1), xyz(q2), qo, qd, kTMin, best, id, best_id, any, t)) {
-                                best = t;
-                                best_id = id;
-                                if (any) { cur = LdsStack16::kSent; break; }
-                            }
-                        }
-                        if (any && best_id >= 0) { leaf = 0; break; }
-                        leaf = cur;
-                        if (cur < 0) {
-                            cur = stk.get(sp);
-                            --sp;
-                        }
-                        if (__popcll(__ballot(leaf < 0)) <= (uint32_t)le) break;
-                    }
-                }
-                // watchdog (traverse_ww4's): rounds of one iteration's loop, ends every query
-                if (++rounds > P.guard_trips) {
-                    if (lane == 0) atomicOr(P.fault, 1);
-                    cur = LdsStack16::kSent;
-                    leaf = 0;
-                    s_more = false;
-                }
-                const bool fin = act && cur == LdsStack16::kSent && leaf >= 0;
-                if (fin) {
-                    bool h = best_id >= 0;
-                    int bid = best_id;
-                    float bt = best;   // t_max when nothing was hit
-                    if (!PLAIN && P.n_sph > 0 && !(any && h)) {
-                        for (int k = 0; k < P.n_sph; ++k) {
-                            float root;
-                            if (sphere_hit(P.sph[k], qo, qd, kTMin, bt, root)) {
-                                bt = root;
-                                bid = P.n_tri + k;
-                                h = true;
-                                if (any) break;
-                            }
-                        }
-                    }
-                    if (STATS) cn.max_q = max(cn.max_q, cn.nodes - cn.q0);
-                    if (s_act) {
-                        // the answer travels back in the owner's t_max word: NaN = occluded
-                        pool[6 * kBlock + s_own] = h ? __int_as_float(0x7FC00000) : 0.0f;
-                    } else {
-                        hid = h ? bid : -1;
-                        ht = bt;
-                        hit = h;
-                    }
-                }
-                const uint64_t ms = __ballot(fin && s_act);
-                if (fin) { e_act = false; s_act = false; }
-                if (ms) {
-                    if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) lanes_s += (uint64_t)__popcll(ms);
-                    // publish the answers before counting them
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == __builtin_amdgcn_readfirstlane(lane))
-                        __hip_atomic_fetch_add(&ctl[9 + slot_prev], (uint32_t)__popcll(ms), __ATOMIC_RELEASE,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
-                if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_s++;
-            }
-            if (STATS) book_trav(0);
-            // the own extension ray again: origin from the pool slot, direction wi (neither stayed in
-            // registers across the shadow queries this lane ran)
-            o = v3(pool[0 * kBlock + tid], pool[1 * kBlock + tid], pool[2 * kBlock + tid]);
-            d = wi;
-        } else if (__ballot(trav) != 0) {
+        if (__ballot(trav) != 0) {
             if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_e++;
-            if constexpr (PK != 0) {
-                // packed leaf trips: every lane of the wave takes part (lanes without a query test
-                // the others' triangles)
-                if (STATS && trav) { cn.ext++; cn.q0 = cn.nodes; }
-                hit = traverse_pk<STATS, false, PK>(g_nodes, g_tris, o, d, kTMax, trav, stk, wb, hid, ht, cn, P.fault,
-                                                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit,
-                                                    P.guard_trips) &&
-                      trav;
-                if (STATS) { if (trav) cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
-            }
             if (trav) {
-                if constexpr (PK == 0) {
-                    if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
-                    hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
-                        g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
-                        exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                    if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
-                }
+                if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
+                hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
+                    g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
+                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
                 if (!PLAIN && P.n_sph > 0) {
                     float best = hit ? ht : kTMax;
                     for (int k = 0; k < P.n_sph; ++k) {
@@ -2127,10 +1689,9 @@ void trace_kernel_pool(TraceParams P) {
             }
         }
         PRT_CLOCK(5);
-        // (b) the previous S phase's answers (its waves ran it beside this wave's traversal; FUSED: the
-        // block's traversals of this iteration): a wave with a pending shadow ray waits until every
-        // chunk (FUSED: every ray) of the previous queue has been answered
-        if (SPLIT ? it_k > 0 : __ballot(my_sh) != 0) {
+        // (b) the previous S phase's answers (its waves ran it beside this wave's traversal): a wave
+        // with a pending shadow ray waits until every chunk of the previous queue has been answered
+        if (__ballot(my_sh) != 0) {
             // bounded: a wait that never ends (a logic error) raises the watchdog flag instead of
             // hanging the device: 2^20 sleeps of 64 clocks ~ 30 ms, against a worst case of ~0.1 ms for
             // the answers (an LDS scene is <= 24 KiB: a query visits each of its <= ~100 nodes and
@@ -2138,28 +1699,7 @@ void trace_kernel_pool(TraceParams P) {
             // did not arrive ends with NaN radiance (counted by STATS' non-finite samples), so a tripped
             // wait cannot pass for a valid image even before prt_check_faults reports it.
             bool late = false;
-            if constexpr (SPLIT) {
-                // every wave: until all four arrived at the previous iteration; a wave with pending
-                // shadow rays: until every chunk of that queue is answered, answering chunks itself
-                const bool need_done = __ballot(my_sh) != 0;
-                for (uint32_t spin = 0;; ++spin) {
-                    if (ld_acq(3 + (int)slot_prev) >= 4u) {
-                        if (!need_done) break;
-                        const uint32_t nch = (ld_rlx((int)slot_prev) + 63u) >> 6;
-                        if (ld_acq(9 + (int)slot_prev) >= nch) break;
-                        if (claim_run(slot_prev, qpar_prev)) continue;
-                    }
-                    if (spin >= (1u << 20)) {
-                        // a wave that never arrives (a logic error): flag it and let the block end
-                        // without the ghost count (bit 8 of word 12)
-                        if (lane == 0) { atomicOr(P.fault, 2); atomicOr(&ctl[12], 0x100u); }
-                        late = true;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            } else {
-            const uint32_t need = FUSED ? nq_prev : nch_prev;
+            const uint32_t need = nch_prev;
             for (uint32_t spin = 0;
                  need && __hip_atomic_load(&ctl[9 + slot_prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need;
                  ++spin) {
@@ -2169,7 +1709,6 @@ void trace_kernel_pool(TraceParams P) {
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-            }
             }
             if (my_sh) {
                 if (STATS) book(14);
@@ -2332,45 +1871,18 @@ void trace_kernel_pool(TraceParams P) {
                 if (my_sh) queue[qpar * kBlock + base + rank] = (uint8_t)tid;
             }
             // a wave with busy lanes or unclaimed work keeps the block looping
-            if (!SPLIT && (__ballot(item >= 0) != 0 || !exhausted) && lane == 0) ctl[3 + slot] = 1u;
+            if ((__ballot(item >= 0) != 0 || !exhausted) && lane == 0) ctl[3 + slot] = 1u;
             // the next iteration's words, last used two iterations ago (every wave has read them since)
             if (tid == 0) {
                 const uint32_t ns = slot == 2 ? 0u : slot + 1u;
                 ctl[ns] = 0u; ctl[3 + ns] = 0u; ctl[6 + ns] = 0u; ctl[9 + ns] = 0u;
             }
         }
-        if constexpr (SPLIT) {
-            // no barrier: count this wave as arrived (after its queue entries, pool slots and the reset
-            // above); a wave with no work left and none to come counts as a ghost once, and the block
-            // ends once a ghost sees all four waves as ghosts before arriving (every wave still waiting
-            // on this iteration has then arrived, and reads four ghosts at its next arrival at the latest)
-            if (!ghost && exhausted && __ballot(item >= 0) == 0) {
-                ghost = true;
-                if (lane == 0) atomicAdd(&ctl[12], 1u);
-            }
-            const uint32_t gw = ld_acq(12);
-            const bool leave = ghost && ((gw & 0xFFu) >= 4u || (gw & 0x100u) != 0u);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_fetch_add(&ctl[3 + slot], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            ++it_k;
-            slot_prev = slot;
-            slot = slot == 2 ? 0u : slot + 1u;
-            qpar_prev = qpar;
-            qpar ^= 1u;
-            o = v3(pool[0 * kBlock + tid], pool[1 * kBlock + tid], pool[2 * kBlock + tid]);
-            d = wi;
-            if (leave) break;
-            continue;
-        }
         PRT_CLOCK(0);
         __syncthreads();
         PRT_CLOCK(1);
         // ------------------------------------------------------------------ S phase
         const uint32_t n_q = ctl[slot];
-        if constexpr (FUSED) {
-            // no S phase: the next iteration's traversals answer this queue
-            nq_prev = n_q;
-        } else {
         // the queue's rays in ceil(n / 64) chunks, one to each of the first waves to claim one (<= 4
         // chunks, one claim per wave); the others refill the lanes that finished in E meanwhile,
         // off the critical path
@@ -2399,27 +1911,14 @@ void trace_kernel_pool(TraceParams P) {
                 sd = v3(pool[3 * kBlock + owner], pool[4 * kBlock + owner], pool[5 * kBlock + owner]);
                 stm = pool[6 * kBlock + owner];
             }
-            bool s_hit = false;
-            if constexpr (PK != 0) {
-                int hid = -1;
-                float ht = 0.0f;
-                if (STATS) cn.q0 = cn.nodes;
-                s_hit = traverse_pk<STATS, true, PK>(g_nodes, g_tris, so, sd, stm, sq, stk, wb, hid, ht, cn, P.fault,
-                                                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit,
-                                                     P.guard_trips);
-                if (STATS) { if (sq) cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
-            }
             if (sq) {
                 int hid = -1;
                 float ht = 0.0f;
-                bool hit = s_hit;
-                if constexpr (PK == 0) {
-                    if (STATS) cn.q0 = cn.nodes;
-                    hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
-                        g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
-                        exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
-                    if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
-                }
+                if (STATS) cn.q0 = cn.nodes;
+                bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
+                    g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
+                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
                 if (!PLAIN && P.n_sph > 0 && !hit) {
                     for (int k = 0; k < P.n_sph; ++k) {
                         float root;
@@ -2435,12 +1934,10 @@ void trace_kernel_pool(TraceParams P) {
             if (lane == 0) __hip_atomic_fetch_add(&ctl[9 + slot], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         nch_prev = n_chunks;
-        }   // !FUSED
         PRT_CLOCK(2);
         const bool alive = ctl[3 + slot] != 0u;
         slot_prev = slot;
         slot = slot == 2 ? 0u : slot + 1u;
-        qpar_prev = qpar;
         qpar ^= 1u;
         // the next extension ray: origin from the pool slot, direction wi (no register keeps the
         // previous ray across the S phase, where the lane may traverse another lane's ray)
@@ -2493,7 +1990,7 @@ void trace_kernel_pool(TraceParams P) {
 }  // namespace
 
 // variant table: (VAR bits of trace_kernel, LDS-resident scene, min waves per SIMD); see prt_kernels.h
-// (bit 512: the block-pooled shadow-query kernel trace_kernel_pool; bit 1024: its FUSED schedule)
+// (bit 512: the block-pooled shadow-query kernel trace_kernel_pool)
 #define PRT_VARIANTS(X)                       \
     X(kVarLds, 8, true, 7)                    \
     X(kVarLdsAnyOcc, 8, true, 1)              \
@@ -2502,18 +1999,7 @@ void trace_kernel_pool(TraceParams P) {
     X(kVarLds6, 8, true, 6)                   \
     X(kVarGlobalMis, 480, false, 6)           \
     X(kVarLdsPool, 512, true, 7)              \
-    X(kVarLdsPool6, 512, true, 6)             \
-    X(kVarLdsFused, 1536, true, 7)            \
-    X(kVarLdsFused6, 1536, true, 6)           \
-    X(kVarLdsPack, 2560, true, 7)             \
-    X(kVarLdsPack6, 2560, true, 6)            \
-    X(kVarLdsSplit, 4608, true, 7)            \
-    X(kVarLdsSplit6, 4608, true, 6)
-
-// the pool kernel's schedule of a variant's bits: 1024 FUSED, 2048 packed leaf trips, 4096 split arrival
-constexpr int pool_sched(int bits) {
-    return (bits & 1024) ? kPoolFused : (bits & 2048) ? kPoolPacked : (bits & 4096) ? kPoolSplit : kPoolTwoPhase;
-}
+    X(kVarLdsPool6, 512, true, 6)
 
 // spill variants exist with LDS stacks of 4 (tests), 16 and 32 entries; the others with 10/16/32
 template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
@@ -2522,7 +2008,7 @@ static hipError_t launch_one(const TraceParams& P, int grid, size_t smem, hipStr
     if constexpr ((VAR & 512) != 0) {
         // the pool kernel's LDS stack size is a launch parameter (P.lds_stack): one instantiation,
         // compiled in its own unit (prt_trace_pool.hip, other register-allocation flags)
-        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, pool_sched(VAR), grid, smem, stream);
+        if constexpr (STACK == 16) return launch_trace_pool(P, STATS, WPE, grid, smem, stream);
         else return hipErrorInvalidValue;
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4)) {
         trace_kernel<STACK, STATS, VAR, LDS, WPE><<<grid, kBlock, smem, stream>>>(P);
@@ -2547,7 +2033,7 @@ template <int STACK, bool STATS, int VAR, bool LDS, int WPE>
 static void occ_one(int* n, size_t smem) {
     constexpr bool spill = (VAR & 32) != 0;
     if constexpr ((VAR & 512) != 0) {
-        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, pool_sched(VAR), smem);
+        if constexpr (STACK == 16) *n = trace_occ_pool(STATS, WPE, smem);
     } else if constexpr (spill ? (STACK == 4 || STACK == 16 || STACK == 32) : (STACK != 4))
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(n, trace_kernel<STACK, STATS, VAR, LDS, WPE>, kBlock, smem);
 }

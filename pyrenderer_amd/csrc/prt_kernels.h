@@ -78,22 +78,12 @@ constexpr int kVarLds6 = 6;        // kVarLds built for >= 6 waves/SIMD (80 VGPR
 constexpr int kVarLdsPool = 7;     // LDS-resident scene, block-pooled shadow queries (trace_kernel_pool),
                                    // >= 7 waves/SIMD; the LDS stack size is P.lds_stack
 constexpr int kVarLdsPool6 = 8;    // kVarLdsPool built for >= 6 waves/SIMD (80 VGPRs)
-constexpr int kVarLdsFused = 9;    // trace_kernel_pool FUSED (round 5): the extension traversals' idle lanes
-                                   // answer the previous iteration's pooled shadow rays; no S phase
-constexpr int kVarLdsFused6 = 10;  // kVarLdsFused built for >= 6 waves/SIMD
-constexpr int kVarLdsPack = 11;    // trace_kernel_pool, two-phase, packed leaf trips (round 5): the triangle
-                                   // tests of all leaves the wave's lanes hold run 64 to a trip (traverse_pk)
-constexpr int kVarLdsPack6 = 12;   // kVarLdsPack built for >= 6 waves/SIMD
-constexpr int kVarLdsSplit = 13;   // trace_kernel_pool, two-phase without the block barrier (round 5): waves
-                                   // arrive per iteration and answer the shadow chunks they wait for
-constexpr int kVarLdsSplit6 = 14;  // kVarLdsSplit built for >= 6 waves/SIMD
 constexpr int kVarFirst = 1;
-constexpr int kVarLast = 14;
-// trace_kernel_pool schedules
-constexpr int kPoolTwoPhase = 0, kPoolFused = 1, kPoolPacked = 2, kPoolSplit = 3;
+constexpr int kVarLast = 8;
+// ids 9-14 were the round-5 schedules of trace_kernel_pool that did not become the default (fused,
+// packed leaf trips, split arrival; DESIGN.md §9, logs in profiles/r05/{fused,pack,split}/): removed
+// in round 6, the C-ABI rejects them as unknown variants
 bool variant_pool(int var);
-bool variant_pack(int var);
-bool variant_split(int var);
 bool variant_mis(int var);
 bool variant_uses_lds(int var);
 bool variant_spills(int var);
@@ -133,10 +123,7 @@ int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 hipError_t launch_rcp_selftest(unsigned long long* d_out, hipStream_t stream);
 // the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
 // the pooled kernel's lean instantiation (no sphere or specular code) runs when P.plain is set
-// (sched: kPoolTwoPhase; kPoolFused, whose extension traversals also answer the previous iteration's
-// shadow rays; kPoolPacked, two-phase with packed leaf trips)
-hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int sched, int grid, size_t smem,
-                             hipStream_t stream);
-int trace_occ_pool(bool stats, int wpe, int sched, size_t smem);
+hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream);
+int trace_occ_pool(bool stats, int wpe, size_t smem);
 
 }  // namespace prt

@@ -252,7 +252,7 @@ size_t trace_smem_bytes(int stack, int var, const TraceParams& P) {
         // trace_kernel_pool: 16-bit stacks of P.lds_stack entries, the shadow pool, queue and control
         // words, then the BVH4 octant copies, triangles and light records (no shading data)
         return (size_t)P.lds_stack * kBlock * sizeof(short) +
-               16 * (size_t)(kPoolF4 + kQueueF4 + kCtlF4 + (variant_pack(var) ? kPkF4 : 0) + (variant_split(var) ? 1 : 0)) +
+               16 * (size_t)(kPoolF4 + kQueueF4 + kCtlF4) +
                16 * (7 * (size_t)P.n_node_f4 + P.n_tri_f4 + 4 * (size_t)P.n_lt + ((size_t)P.n_light + 4) / 4 +
                      2 * (size_t)P.n_mat);
     }
@@ -389,24 +389,6 @@ bool variant_spills(int var) {
 bool variant_pool(int var) {
     switch (var) {
 #define X(id, bits, lds, wpe) case id: return (bits & 512) != 0;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
-
-bool variant_pack(int var) {
-    switch (var) {
-#define X(id, bits, lds, wpe) case id: return (bits & 2048) != 0;
-        PRT_VARIANTS(X)
-#undef X
-        default: return false;
-    }
-}
-
-bool variant_split(int var) {
-    switch (var) {
-#define X(id, bits, lds, wpe) case id: return (bits & 4096) != 0;
         PRT_VARIANTS(X)
 #undef X
         default: return false;

@@ -22,10 +22,15 @@ class TileShard:
     `bufs[f]` holds the rank's per-tile radiance sums of frame f (of `frames`, the frames one
     render call produces: DeviceScene.render_frames_device) on `device`; `buf` is frame 0.  With
     `host_staging` (the gloo backend, which moves CPU tensors) gather() first copies them to host
-    memory."""
+    memory.
 
-    def __init__(self, W, H, tile, rank, world, device, scheme="latin", host_staging=False, frames=1):
+    `collective`: take the gather / root-scatter path even at world 1 (bench.py --force-collective:
+    a one-rank process group runs the N > 1 step's RCCL code on one GPU); world > 1 always does."""
+
+    def __init__(self, W, H, tile, rank, world, device, scheme="latin", host_staging=False, frames=1,
+                 collective=False):
         self.W, self.H, self.tile, self.rank, self.world = W, H, tile, rank, world
+        self.coll = world > 1 or bool(collective)
         self.scheme = scheme
         self.frames = int(frames)
         tx, ty = tile_grid(W, H, tile)
@@ -41,7 +46,7 @@ class TileShard:
         self.host_staging = bool(host_staging) and self.buf.is_cuda
         self.wire = torch.empty_like(self.bufs, device="cpu") if self.host_staging else self.bufs
         self.gathered = None
-        if world > 1 and rank == 0:
+        if self.coll and rank == 0:
             # one contiguous receive buffer [rank][frame][slots]: a group's frames arrive in ONE
             # gather, and frame f's tiles of every rank sit at the same offsets from
             # gathered[0, f], rank r's block a stride of frames * max_tiles tiles further on
@@ -63,13 +68,14 @@ class TileShard:
 
     def gather(self, group=None, n_frames=1):
         """Collective: rank 0 receives every rank's tile sums of frames 0 .. n_frames-1 in ONE
-        gather (no-op for world 1).  Runs on torch's current stream: callers that rendered on
+        gather.  Runs on torch's current stream: callers that rendered on
         another stream enter it first (ProcessGroupNCCL's collective stream waits for the current
         one when the gather is enqueued, so the send follows the render).  The receive side is
         ordered explicitly: the gather is issued asynchronously and its work's wait() makes the
         current stream wait for the collective stream (nccl; gloo: the host waits), so a
-        scatter_frames() enqueued next on this stream reads the received tiles."""
-        if self.world > 1:
+        scatter_frames() enqueued next on this stream reads the received tiles.  No-op without the
+        collective path (world 1)."""
+        if self.coll:
             if self.host_staging:
                 self.wire[:n_frames].copy_(self.bufs[:n_frames])   # synchronous device-to-host copy
             work = dist.gather(self.wire[:n_frames], self.gather_list(n_frames), dst=0, group=group, async_op=True)
@@ -89,7 +95,7 @@ class TileShard:
         with torch.cuda.stream(s):
             if self.frame_out is None:
                 self.frame_out = torch.zeros((self.frames, self.W, self.H, 3), dtype=torch.float32, device=dev)
-            if self.world == 1:
+            if not self.coll:
                 packed, ids, group_pitch = self.bufs, self.per_rank[0], 0
             else:
                 packed = self.gathered
@@ -99,7 +105,7 @@ class TileShard:
                     self.packed_dev.copy_(self.gathered)
                     packed = self.packed_dev
                 ids, group_pitch = self.scatter_ids, self.frames * self.pitch
-        group_tiles = self.max_tiles if self.world > 1 else max(len(ids), 1)
+        group_tiles = self.max_tiles if self.coll else max(len(ids), 1)
         if len(ids):
             device_scene.scatter_frames(packed.data_ptr(), ids, group_tiles, group_pitch, self.tile, self.tile, self.W,
                                         self.H, n_frames, self.pitch, self.frame_out.data_ptr(), s.cuda_stream)
@@ -117,7 +123,7 @@ class TileShard:
             # scatter overwrites
             if self.frame_out is None:
                 self.frame_out = torch.zeros((self.frames, self.W, self.H, 3), dtype=torch.float32, device=dev)
-            if self.world == 1:
+            if not self.coll:
                 base, ids, group_pitch = self.bufs[f], self.per_rank[0], 0
             else:
                 packed = self.gathered
@@ -128,7 +134,7 @@ class TileShard:
                         self.packed_dev.copy_(self.gathered)
                     packed = self.packed_dev
                 base, ids, group_pitch = packed[0, f], self.scatter_ids, self.frames * self.pitch
-        group_tiles = self.max_tiles if self.world > 1 else max(len(ids), 1)
+        group_tiles = self.max_tiles if self.coll else max(len(ids), 1)
         if len(ids):
             device_scene.scatter_frames(base.data_ptr(), ids, group_tiles, group_pitch, self.tile, self.tile, self.W,
                                         self.H, 1, self.pitch, self.frame_out[f].data_ptr(), s.cuda_stream)
@@ -141,7 +147,7 @@ class TileShard:
         the frame — the gathered tiles never pass through a host loop.  Without it (CPU-tensor
         shards: the gloo tests with the CPU oracle as renderer) the tiles are unpacked in numpy."""
         if device_scene is None:
-            bufs = [self.gathered[r, f] for r in range(self.world)] if self.world > 1 else [self.bufs[f]]
+            bufs = [self.gathered[r, f] for r in range(self.world)] if self.coll else [self.bufs[f]]
             frame = np.zeros((self.W, self.H, 3), np.float32)
             for b, ids in zip(bufs, self.per_rank):
                 n = len(ids) * self.slot_elems
@@ -149,7 +155,7 @@ class TileShard:
             return frame
         dev = torch.device("cuda", device_scene.device)
         s = stream or torch.cuda.current_stream(dev)
-        if self.world > 1 and not self.gathered.is_cuda and f != 0:
+        if self.coll and not self.gathered.is_cuda and f != 0:
             self.scatter(device_scene, s, 0)    # uploads the gloo host buffer for this group
         frame = self.scatter(device_scene, s, f)
         with torch.cuda.stream(s):

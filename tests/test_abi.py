@@ -22,7 +22,7 @@ def test_library_exports_header_symbols():
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(N.EXPORTS), set(names) ^ set(N.EXPORTS)
-    assert L.prt_abi_version() == N.ABI_VERSION == 3
+    assert L.prt_abi_version() == N.ABI_VERSION == 4
 
 
 def test_device_count_without_gpu_is_ok():
@@ -38,6 +38,19 @@ def test_errors_are_reported():
     assert rc == -1 and b"NULL" in N.lib().prt_last_error()
     with pytest.raises(N.PrtError):
         N.Bvh(np.zeros((2, 9), np.float32), max_leaf=0)
+
+
+def test_scatter_frames_rejects_overlapping_groups():
+    """with several groups, a group_pitch shorter than its n_frames frames at src_frame_pitch
+    would let frame f of group g read group g + 1's block; the shape check rejects it before any device
+    work (no scene or GPU needed to reach it)."""
+    from pyrenderer_amd import _native as N
+    L = N.lib()
+    ids = np.zeros(2, np.int32)
+    slot = 16 * 16 * 3
+    # 2 groups of 1 tile, 2 frames at a pitch of one slot: a group needs 2 slots
+    rc = L.prt_scatter_frames(None, None, N.ptr(ids), 2, 1, slot, 16, 16, 32, 32, 2, slot, None, None)
+    assert rc == -1 and b"n_frames frames" in L.prt_last_error()   # PRT_ERR_ARG
 
 
 def _traverse_py(nodes, tris, order, ro, rd, tmin, tmax):

@@ -85,6 +85,12 @@ def test_launch_check_spawns_the_launcher_as_a_child(monkeypatch):
     # one GPU, or already under a launcher with the matching world size: render in this process
     assert bench.launch_check(_args(monkeypatch, []), env={}) is None
     assert bench.launch_check(args, env={"WORLD_SIZE": "2"}) is None
+    # --force-collective at one GPU: a one-rank launcher, then the collective path
+    fc = _args(monkeypatch, ["--force-collective", "--steps", "3"])
+    assert fc.force_collective and fc.gpus == 1
+    assert bench.launch_check(fc, env={"PATH": "/usr/bin"}) == 7
+    assert "--nproc-per-node=1" in seen["cmd"] and seen["cmd"][-3:] == ["--force-collective", "--steps", "3"]
+    assert bench.launch_check(fc, env={"WORLD_SIZE": "1"}) is None
 
 
 def _run_bench(argv, **env):

@@ -62,14 +62,15 @@ def test_gather_matches_single_process(tmp_path, world, W, H):
     assert frame.sum() > 0
 
 
-def _frames_worker(rank, world, port, out_path, n_frames):
+def _frames_worker(rank, world, port, out_path, n_frames, coll=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import sys
     sys.path.insert(0, ROOT)
     from pyrenderer_amd.distributed import TileShard
-    shard = TileShard(W, H, TILE, rank, world, torch.device("cpu"), frames=n_frames)
+    shard = TileShard(W, H, TILE, rank, world, torch.device("cpu"), frames=n_frames, collective=coll)
+    assert shard.coll == (world > 1 or coll) and (shard.gathered is not None) == (rank == 0 and shard.coll)
     # frame f's sums of pixel (x, y): a value that names both, so a mixed-up frame or tile shows
     n = len(shard.tiles) * TILE * TILE
     for f in range(n_frames):
@@ -87,13 +88,15 @@ def _frames_worker(rank, world, port, out_path, n_frames):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_multi_frame_gathers(tmp_path, world):
+@pytest.mark.parametrize("world, coll", [(1, True), (2, False), (3, False)])
+def test_multi_frame_gathers(tmp_path, world, coll):
     """bench.py's multi-frame groups: F frames' tile sums per rank, one gather per frame, each
-    frame assembled from its own gathered buffer."""
+    frame assembled from its own gathered buffer.  World 1 with `collective` is bench.py
+    --force-collective's path: a one-rank group still gathers into rank 0's buffer and assembles
+    from it."""
     out = str(tmp_path / "frames.npy")
     F = 3
-    mp.spawn(_frames_worker, args=(world, _free_port(), out, F), nprocs=world, join=True)
+    mp.spawn(_frames_worker, args=(world, _free_port(), out, F, coll), nprocs=world, join=True)
     frames = np.load(out)
     assert frames.shape == (F, W, H, 3)
     x, y = np.meshgrid(np.arange(W), np.arange(H), indexing="ij")

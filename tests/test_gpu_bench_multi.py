@@ -81,3 +81,29 @@ def test_bench_three_ranks_ragged_multi_frame_over_gloo():
     assert three["n_gpus"] == 3 and three["config"]["frames_per_launch"] == 4
     assert len(three["config"]["ranks"]) == 3 and len(three["rank_ms_per_step"]["per_rank"]) == 3
     assert three["l2_vs_cpu"]["identical_pixels"] == 1.0
+
+
+@pytest.mark.timeout(400)
+def test_bench_force_collective_nccl_world_one():
+    """the RCCL branch of the N > 1 step, executed on the one GPU.  `bench.py --gpus 1
+    --backend nccl --force-collective` starts torch.distributed.run with ONE rank itself, runs
+    init_process_group("nccl", device_id=dev), the device-tensor all_gather_object / all_reduce / all_gather,
+    the async dist.gather of every multi-frame group into rank 0's DEVICE `gathered` buffer with
+    work.wait() ordering the stream, and prt_scatter_frames from that buffer — the code the driver's 8-GPU
+    line runs, minus the xGMI transport between distinct GPUs.  The gathered frame of a timed group must
+    equal the CPU oracle bit for bit."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    args = ["--res", "128", "--spp", "8", "--depth", "8", "--tile", "16", "--steps", "8", "--warmup", "1",
+            "--numpy-seconds", "0", "--cpu-seconds", "2", "--frames-per-launch", "4", "--single-frame-steps", "2"]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--backend", "nccl", "--force-collective"] + args,
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = _line(r.stdout)
+    c = line["config"]
+    assert line["n_gpus"] == 1 and c["backend"] == "nccl" and c["collective"] is True
+    assert len(c["ranks"]) == 1 and c["ranks"][0]["rank"] == 0 and c["frames_per_launch"] == 4
+    l2 = line["l2_vs_cpu"]
+    assert l2["source"] == "timed group" and l2["gathered"] is True and l2["frames_per_launch"] == 4
+    assert l2["identical_pixels"] == 1.0 and l2["rmse"] == 0.0 and l2["pass"]
+    assert line["single_frame"]["ms_per_step"] > 0 and line["value"] > 0

@@ -46,3 +46,22 @@ def test_camera_kernel_rays_equal_host_gen_ray(gpu_scene, cornell, mod):
     assert go.shape == ho.shape == (4096, 3)
     np.testing.assert_array_equal(gd, hd)
     np.testing.assert_array_equal(go, ho)
+
+
+def test_camera_rays_of_partial_edge_tiles(gpu_scene, cornell):
+    """a frame whose size is not a multiple of the tile (40 x 36, 16-pixel tiles): rows of
+    slots whose pixel lies outside the frame come back as zeros (origin, RNG state and direction — the
+    camera kernel gives them no ray), the in-frame rows still equal the host gen_ray.  Also keys each
+    sample as enqueue_render does (frame_spp = spp, frame_stride = 0)."""
+    pc = cornell[1].convert_to_taichi_camera()
+    W, H, tile, spp, seed = 40, 36, 16, 3, 5
+    tiles = list(range(9))                              # 3 x 3 tiles, the last row and column partial
+    go, gd, gs = gpu_scene.camera_rays(pc.packed(), W, H, tile, tile, tiles, 0, spp, seed=seed)
+    ho, hd = _host_rays(pc, W, H, tile, tiles, spp, seed, False)
+    tx = (W + tile - 1) // tile
+    inside = np.array([((t % tx) * tile + r % tile < W) and ((t // tx) * tile + r // tile < H)
+                       for _ in range(spp) for t in tiles for r in range(tile * tile)])
+    assert inside.sum() == W * H * spp and (~inside).sum() > 0
+    np.testing.assert_array_equal(gd[inside], hd[inside])
+    np.testing.assert_array_equal(go[inside], ho[inside])
+    assert not go[~inside].any() and not gd[~inside].any() and not gs[~inside].any()

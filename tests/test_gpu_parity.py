@@ -248,9 +248,9 @@ def test_specular_scene_matches_oracle(rough, kernel):
 
 
 def test_pool_variants_identical_on_the_specular_scene():
-    """Every schedule of the pooled kernel's full build (spheres, metal, dielectric: two-phase, fused,
-    packed leaf trips, split arrival; 7 and 6 waves per SIMD) renders the same bits on config 3's
-    materials, and those bits match the oracle as test_specular_scene_matches_oracle requires."""
+    """Both builds of the pooled kernel's full instantiation (spheres, metal, dielectric; 7 and 6 waves
+    per SIMD) render the same bits on config 3's materials, and those bits match the oracle as
+    test_specular_scene_matches_oracle requires."""
     from pyrenderer_amd import _native as N
     from pyrenderer_amd.device_scene import DeviceScene
     scene, cam, flat = _specular_scene(0.35)
