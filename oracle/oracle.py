@@ -18,7 +18,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "libprt_oracle.so")
+# PRT_ORACLE_LIB: another build of the same source (tools/sanitize: AddressSanitizer + UBSan)
+_LIB_PATH = os.environ.get("PRT_ORACLE_LIB") or os.path.join(_HERE, "_build", "libprt_oracle.so")
 
 BACKEND_REF = 0     # reference structure: median-split BVH over primitives + per-primitive loop
 BACKEND_BRUTE = 1   # all triangles, closest (t, index)

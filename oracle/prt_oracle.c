@@ -948,6 +948,9 @@ OR_API void or_closest_batch(void* p, int backend, int64_t n, const float* ro, c
                              const float* t0, const float* t1, int32_t* out_hit, float* out_t,
                              int64_t* out_tri, float* out_n) {
     OScene* s = (OScene*)p;
+    /* independent rays, read-only scene: OpenMP over the batch (the brute-force backend's 1 M-triangle
+     * checks of config 4, tests/test_gpu_configs.py) */
+#pragma omp parallel for schedule(dynamic, 8)
     for (int64_t i = 0; i < n; ++i) {
         Hit h = closest_hit(s, backend, ld3(ro + 3 * i), ld3(rd + 3 * i), t0[i], t1[i], NULL);
         out_hit[i] = h.hit; out_t[i] = h.t; out_tri[i] = h.hit ? h.tri : -1;

@@ -44,7 +44,11 @@ def parse(argv=None):
                     help="also save the reference's HDR pair (main_taichi.py:120-123) into DIR: hdr.npy = the "
                          "radiance sums (W, H, 3) [x][y], spp.npy = the per-pixel sample counts (W, H); "
                          "the reference's tone_map.py reads exactly these")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.hdr and args.hdr.lower().endswith(".npy"):
+        # rounds <= 4 took a .npy FILE here; a directory named out.npy would silently replace it
+        ap.error(f"--hdr takes a directory (hdr.npy and spp.npy are written into it), not a .npy file: {args.hdr}")
+    return args
 
 
 def _write(args, sums, samples, mean):

@@ -144,8 +144,10 @@ def test_config4_hits_match_oracle(cubes, quantized):
     assert (gid[gid >= 0] < 1_000_008).mean() > 0.5
     o, d = _axis_rays(600, 12, lo=(-0.99, 0.01, -0.99), hi=(0.99, 1.97, 0.99))
     check(o, d)
-    o, d = _cube_rays(300, 13)
-    check(o, d, backend=O.BACKEND_BRUTE)
+    # the frame test's oracle walks the library-built BVH, so the tree is pinned here
+    # by brute force over all 1 M triangles (OpenMP in the oracle)
+    o, d = _cube_rays(2000, 13)
+    assert check(o, d, backend=O.BACKEND_BRUTE) > 0.9
     # bounded (shadow-style) any-hit queries
     o, d = _cube_rays(20000, 14)
     tmax = np.random.default_rng(15).uniform(0.001, 0.3, o.shape[0]).astype(np.float32)

@@ -28,3 +28,14 @@ def test_hdr_pair_reproduces_finish_of_the_mean(tmp_path):
     np.testing.assert_array_equal(ldr1, finish(mean))
     np.testing.assert_array_equal(finish_hdr(hdr_mat, spp_mat), ldr1)
     assert np.array_equal(hdr_mat[~np.isnan(hdr_mat)], sums[~np.isnan(sums)])   # the sums themselves
+
+
+def test_cli_rejects_an_npy_file_for_the_hdr_directory(capsys):
+    """`--hdr out.npy` (the pre-round-5 file form) is refused instead of silently creating a
+    directory named out.npy."""
+    import pytest
+    from pyrenderer_amd.main import parse
+    assert parse(["--hdr", "outdir"]).hdr == "outdir"
+    with pytest.raises(SystemExit) as e:
+        parse(["--hdr", "out.npy"])
+    assert e.value.code == 2 and "directory" in capsys.readouterr().err
