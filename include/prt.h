@@ -42,7 +42,7 @@ extern "C" {
  * ABI 4 (this build, round 6): variant ids 9..14 removed again (none became the default; DESIGN.md
  * §9), ids above 8 are rejected with PRT_ERR_ARG as in ABI 2; prt_scatter_frames rejects a
  * group_pitch too short for n_frames frames at src_frame_pitch; prt_camera_rays zero-fills the rows
- * of slots outside the frame. */
+ * of slots outside the frame; prt_selftest_guards added. */
 #define PRT_ABI_VERSION 4
 
 #define PRT_OK 0
@@ -237,6 +237,14 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches);
  * 3 [2^-40, 2^40] (the range the kernels use the sequence in), 4 (2^40, 2^126], 5 > 2^126 finite,
  * 6 infinite, 7 NaN (both results NaN count as equal).  ABI 3, round 5. */
 int prt_selftest_rcp(int device, uint64_t* mismatches8);
+/* ABI 4: the guards of the kernels' fast sequences, swept over all 2^32 floats b on `device`
+ * (counts16, 10 used): 0 rcp_fast_seq mismatches against 1.0f / b that its guard accepts (the result
+ * is a normal float) — the kernels rely on this being 0; 1 operands that guard sends to the division;
+ * 2 all rcp mismatches; 3 rcp mismatches for normal |b| <= 2^126; 4 sqrt_fast_seq mismatches against
+ * sqrtf that its guard accepts (b >= 2^-96) — must be 0; 5 operands sent to sqrtf; 6 all sqrt
+ * mismatches; 7 sqrt mismatches in [2^-96, FLT_MAX]; 8 for +0 and normal b < 2^-96; 9 for denormal b
+ * (NaN results count as equal). */
+int prt_selftest_guards(int device, uint64_t* counts16);
 /* Failure detection for renders whose result stays on the device (prt_render_tiles_device,
  * the torch.distributed path): synchronises the device, then reports PRT_ERR_INTERNAL if
  * the traversal watchdog tripped in the last render enqueued on any of this scene's

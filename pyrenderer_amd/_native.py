@@ -78,6 +78,7 @@ EXPORTS = {
     "prt_render_tiles_accumulate": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _u64, _u32, _vp]),
     "prt_kernel_timing": (_i, [_vp, _vp, _vp]),
     "prt_selftest_rcp": (_i, [_i, _vp]),
+    "prt_selftest_guards": (_i, [_i, _vp]),
     "prt_check_faults": (_i, [_vp]),
     "prt_last_stats": (_i, [_vp, _vp]),
     "prt_diag_stats": (_i, [_vp, _vp]),

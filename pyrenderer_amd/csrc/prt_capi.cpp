@@ -133,6 +133,7 @@ struct Scene {
     std::string wave_clock_path;     // env PRT_WAVE_CLOCK: append each trace launch's per-wave clocks here
     int64_t n_sph = 0;
     bool plain = false;              // no spheres, no metal / dielectric material (TraceParams::plain)
+    bool shade_fast = false;         // TraceParams::shade_fast (prt_scene_create)
     DevBuf work, stats;              // work: hit-query watchdog flag; stats: PRT_FLAG_STATS counters
     hipStream_t stream = nullptr;
     std::vector<std::unique_ptr<RenderCtx>> ctx;  // per render stream (<= kMaxCtx)
@@ -328,6 +329,7 @@ void scene_params(Scene* s, prt::TraceParams& P) {
     P.sph = (const float4*)s->sph.p;
     P.sph_mat = (const int*)s->sph_mat.p;
     P.plain = s->plain ? 1 : 0;
+    P.shade_fast = s->shade_fast ? 1 : 0;
     P.frame_spp = 0xFFFFFFFFu;   // one frame: global sample = s0 + j0 + the chunk's sample
 }
 
@@ -767,6 +769,19 @@ int prt_scene_create(int device, const float* tri_v, const float* tri_n, const i
         s->plain = n_sph == 0;
         for (int32_t i = 0; i < n_mat; ++i)
             if (mat[8 * i + 5] == 2.0f || mat[8 * i + 5] == 3.0f) s->plain = false;   // metal / dielectric
+        // the shading quotients' cheap guards (prt_device.h lambert_div / nee_div) assume albedos and
+        // emitters in [2^-40, 2^40] and face normals of length in [0.5, 2]; other scenes keep div3's guard
+        s->shade_fast = true;
+        for (int32_t i = 0; i < n_mat && s->shade_fast; ++i)
+            for (int c = 0; c < 3; ++c) {
+                const float r = mat[8 * i + c];
+                if (!(r >= 0x1p-40f && r <= 0x1p40f)) s->shade_fast = false;
+            }
+        for (int64_t i = 0; i < n_tri && s->shade_fast; ++i) {
+            const double x = tri_n[3 * i], y = tri_n[3 * i + 1], z = tri_n[3 * i + 2];
+            const double l2 = x * x + y * y + z * z;
+            if (!(l2 >= 0.25 && l2 <= 4.0)) s->shade_fast = false;
+        }
         if ((rc = upload(s->sph, sph, sizeof(float) * 4 * (size_t)n_sph, &s->device_bytes))) break;
         if ((rc = upload(s->sph_mat, sph_mat, sizeof(int32_t) * (size_t)n_sph, &s->device_bytes))) break;
         if ((e = s->work.ensure(64)) != hipSuccess || (e = s->stats.ensure(8 * kStatWords)) != hipSuccess) {
@@ -1141,6 +1156,22 @@ int prt_kernel_timing(void* scene, double* ms_total, int64_t* launches) {
         return fail(PRT_ERR_INTERNAL, "traversal watchdog tripped (corrupt acceleration structure?)");
     }
     s->ev_used = 0;
+    return PRT_OK;
+}
+
+int prt_selftest_guards(int device, uint64_t* counts16) {
+    if (!counts16) return fail(PRT_ERR_ARG, "NULL argument");
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return fail(PRT_ERR_HIP, "no such HIP device");
+    DeviceGuard g(device);
+    DevBuf d;
+    HIP_TRY(d.ensure(16 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(d.p, 0, 16 * sizeof(unsigned long long)));
+    HIP_TRY(prt::launch_guard_selftest((unsigned long long*)d.p, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long h[16];
+    HIP_TRY(hipMemcpy(h, d.p, sizeof(h), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 16; ++i) counts16[i] = h[i];
     return PRT_OK;
 }
 

@@ -93,49 +93,127 @@ __device__ __forceinline__ V3 div3_nan_guard(V3 a, float pdf) {
     if (div_is_nan(a.x, pdf) || div_is_nan(a.y, pdf) || div_is_nan(a.z, pdf)) pdf = 1e-4f;
     return v3(a.x / pdf, a.y / pdf, a.z / pdf);
 }
+// v_cmp_class_f32 masks (one VALU instruction tests any set of IEEE classes)
+constexpr int kClassNegNormal = 1 << 3, kClassPosZero = 1 << 6, kClassPosNormal = 1 << 8;
+constexpr int kClassNormal = kClassNegNormal | kClassPosNormal;
+constexpr int kClassDenorm = (1 << 4) | (1 << 7);
 // 1 / b, correctly rounded: for finite |b| in [2^-40, 2^40] the division expansion (see
 // div3) with numerator 1 is the refined reciprocal plus two quotient corrections
-// (its q = 1 * r is exact); other waves take the plain division.
-// the sequence itself (prt_selftest_rcp compares it with the IEEE division over all 2^32 floats)
+// (its q = 1 * r is exact).
+// the sequence itself (prt_selftest_rcp / prt_selftest_guards compare it with the IEEE division
+// over all 2^32 floats)
 __device__ __forceinline__ float rcp_fast_seq(float b) {
     float r = __builtin_amdgcn_rcpf(b);
     r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
     const float q = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
     return __builtin_fmaf(__builtin_fmaf(-b, q, 1.0f), r, q);
 }
+// The wave's lanes of class mask m, as one v_cmp_class_f32 into an SGPR pair (inactive lanes read 0).
+// Written out because the ballot of llvm.amdgcn.class is lowered through a VGPR (v_cndmask + v_cmp: two
+// more VALU per test), and the mask sits in an SGPR (above 64 it is no inline constant; a VGPR copy
+// pinned across the loops cost the pooled kernel a spill).
+__device__ __forceinline__ uint64_t class_lanes(float x, int m) {
+    uint64_t k;
+    asm("v_cmp_class_f32_e64 %0, %1, %2" : "=s"(k) : "v"(x), "s"(m));
+    return k;
+}
+// rcp_fast_seq's guard, on the RESULT (round 6): whenever the sequence returns a
+// normal float it returns 1.0f / b — proven by the exhaustive sweep over all 2^32 operands on gfx950
+// (prt_selftest_guards counter 0 with this per-lane form, tests/test_gpu_selftest.py); zero, denormal,
+// huge (> 2^126), infinite and NaN operands give a non-normal result and take the division.  One
+// v_cmp_class per test instead of round 5's two range compares on |b|.
+__device__ __forceinline__ bool rcp_guard_ok(float r) { return __builtin_amdgcn_classf(r, kClassNormal); }
 __device__ __forceinline__ float rcp_exact(float b) {
-    const float ab = fabsf(b);
-    if (__ballot(!(ab >= 0x1p-40f && ab <= 0x1p40f)) == 0) return rcp_fast_seq(b);
-    return 1.0f / b;
+    float r = rcp_fast_seq(b);
+    if (class_lanes(r, kClassNormal) != __builtin_amdgcn_read_exec()) {
+        // a real branch: without the (empty, volatile) asm the compiler if-converts the division into
+        // every test (both sequences and a select)
+        asm volatile("");
+        r = 1.0f / b;
+    }
+    return r;
 }
 // Correctly rounded sqrt.  hipcc expands sqrtf on gfx950 as: scale x by 2^32 when
 // x < 2^-96, v_sqrt_f32, correct the result by one ulp down / up from the signs of the
-// residuals fma(-(s -/+ 1 ulp), s, x), unscale, and return x itself for +-0 / +inf.  For
-// finite x in [2^-96, FLT_MAX] the scaling and the class test change nothing, so with FAST
-// a wave whose lanes are all in that range runs the corrected v_sqrt alone (bit-identical);
-// other waves take sqrtf.  FAST is used by the LDS-scene kernels (C2 -0.5 %); the
+// residuals fma(-(s -/+ 1 ulp), s, x), unscale, and return x itself for +-0 / +inf.  With FAST
+// a wave whose operands are all in the guard's domain (below) runs the corrected v_sqrt alone
+// (bit-identical); other waves take sqrtf.  FAST is used by the LDS-scene kernels (C2 -0.5 %); the
 // global-scene kernel keeps sqrtf (its extra live registers cost spills there).
+// the sequence itself (prt_selftest_guards sweeps it over all 2^32 floats against sqrtf)
+__device__ __forceinline__ float sqrt_fast_seq(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u);
+    const float su = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rd = __builtin_fmaf(-sd, s, x);
+    const float ru = __builtin_fmaf(-su, s, x);
+    const float r = rd <= 0.0f ? sd : s;
+    return ru > 0.0f ? su : r;
+}
+// Its guard (round 6): x >= 2^-96, ONE compare instead of round 5's range test
+// [2^-96, FLT_MAX].  The exhaustive sweep over all 2^32 floats (prt_selftest_guards counters 4-9)
+// finds the sequence equal to sqrtf for every operand except the denormals (of either sign) and the
+// operands in [+0, 2^-96), where sqrtf scales: +inf gives +inf on both sides, negative operands and NaN
+// give NaN on both sides, so the upper bound was never needed.
+__device__ __forceinline__ bool sqrt_guard_ok(float x) { return x >= 0x1p-96f; }
 template <bool FAST>
 __device__ __forceinline__ float sqrt_cr(float x) {
     if constexpr (FAST) {
-        if (__ballot(!(x >= 0x1p-96f && x <= 0x1.fffffep127f)) == 0) {
-            const float s = __builtin_amdgcn_sqrtf(x);
-            const float sd = __uint_as_float(__float_as_uint(s) - 1u);
-            const float su = __uint_as_float(__float_as_uint(s) + 1u);
-            const float rd = __builtin_fmaf(-sd, s, x);
-            const float ru = __builtin_fmaf(-su, s, x);
-            const float r = rd <= 0.0f ? sd : s;
-            return ru > 0.0f ? su : r;
-        }
+        if (__ballot(!sqrt_guard_ok(x)) == 0) return sqrt_fast_seq(x);
+        asm volatile("");
     }
     return sqrtf(x);
 }
-// taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt)
+// taichi_glsl normalize: v / length(v) (IEEE division, correctly rounded sqrt).
+// FAST (round 6): the shared-reciprocal quotients under a cheaper guard than div3's — every |a_i| >=
+// 2^-60 and s = length(a) <= 2^64 (four compares, no min / sum chain).  That is
+// div3's no-scaling condition for this quotient: s >= |a_i| (1 - 2^-23) > 2^-61 (s = sqrt(dot) and
+// dot >= each rounded square), so s and 1/s are normal, |a_i / s| <= 1 + 2^-23 (no overflow, exponent
+// difference <= 1 < 96), |a_i / s| >= 2^-124 (normal with two binades of margin), every a_i has a
+// biased exponent >= 67 > 23 and none is zero; an infinite a_i makes s infinite and a NaN fails its
+// compare, so those waves divide.
 template <bool FAST = false>
 __device__ __forceinline__ V3 normalize(V3 a) {
-    return div3(a, sqrt_cr<FAST>(dot(a, a)));
+    const float s = sqrt_cr<FAST>(dot(a, a));
+    if constexpr (FAST) {
+        const bool ok = (int)(fabsf(a.x) >= 0x1p-60f) & (int)(fabsf(a.y) >= 0x1p-60f) &
+                        (int)(fabsf(a.z) >= 0x1p-60f) & (int)(s <= 0x1p64f);
+        if (__ballot(!ok) == 0) return div3_fast(a, s);
+        return v3(a.x / s, a.y / s, a.z / s);
+    }
+    return div3(a, s);
 }
 __device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
+// The Lambert vertex's BRDF weight division (att * max(cw, 0)) / (|cw| / pi) under the reference's NaN
+// rule (tracing.py:146-148; ad = att * dz, pdf = |cw| * InvPi).  FAST (round 6):
+// on a scene whose albedos lie in [2^-40, 2^40] and whose face normals have length in [0.5, 2]
+// (TraceParams::shade_fast, checked on the host), cw >= 2^-60 alone puts the quotient in div3's
+// no-scaling domain: cw <= |n| |wi| <= 2 (wi normalised; sphere normals (p - c) / r ~ 1), so pdf =
+// cw / pi is normal in [2^-62, 1], ad_i = att_i cw in [2^-100, 2^41] (normal, biased exponent >= 27 >
+// 23, non-zero), ad_i / pdf ~ pi att_i in [2^-39, 2^42] (normal, exponent difference <= 42 < 96), and
+// no quotient is NaN, so the rule does not fire: one compare instead of div3's range test (a NaN cw
+// fails it).
+template <bool FAST>
+__device__ __forceinline__ V3 lambert_div(V3 ad, float pdf, float cw, int shade_fast) {
+    if constexpr (FAST) {
+        if (shade_fast && __ballot(!(cw >= 0x1p-60f)) == 0) return div3_fast(ad, pdf);
+    }
+    return div3_nan_guard(ad, pdf);
+}
+// The NEE term's division (em * dot1 * dot2) / |p - p2|^2 (tracing.py:92-108).  FAST (round 6): under
+// shade_fast (above) em_i in [2^-40, 2^40] and dot1, dot2 <= 2 (unit-ish w, normals of length <= 2), so
+// with dot1, dot2 >= 2^-20 and sl in [2^-40, 2^40] the numerators lie in [2^-81, 2^42] (normal, biased
+// exponent >= 46), sl and 1 / sl are normal, the quotients lie in [2^-121, 2^82] and the exponent
+// difference is <= 82 < 96: div3's no-scaling domain with four compares instead of div3's range test.
+template <bool FAST>
+__device__ __forceinline__ V3 nee_div(V3 a, float sl, float dot1, float dot2, int shade_fast) {
+    if constexpr (FAST) {
+        const bool ok = (int)(dot1 >= 0x1p-20f) & (int)(dot2 >= 0x1p-20f) & (int)(sl >= 0x1p-40f) &
+                        (int)(sl <= 0x1p40f);
+        if (shade_fast && __ballot(!ok) == 0) return div3_fast(a, sl);
+    }
+    return div3(a, sl);
+}
+
 
 // ------------------------------------------------------------------ RNG spec
 __device__ __forceinline__ uint32_t pcg_permute(uint32_t s) {
@@ -181,7 +259,22 @@ __device__ __forceinline__ V3 cosine_hemisphere(float u0, float u1) {
         // divergent if/else would run two of each on a wave holding both cases).
         const bool wide = fabsf(ox) > fabsf(oy);
         const float r = wide ? ox : oy;
-        const float t = kPiOver4 * ((wide ? oy : ox) / r);
+        float t;
+        if constexpr (FAST) {
+            // round 6: the quotient by div3's shared-reciprocal sequence, unguarded: u0, u1 are
+            // rng_next draws (multiples of 2^-24 in [0, 1)), so ox, oy = 2u - 1 are exact multiples of
+            // 2^-23 in [-1, 1): |r| >= 2^-23 and the numerator is +0 or of magnitude in [2^-23, |r|] —
+            // div3's no-scaling domain (quotient in [2^-23, 1], biased exponents >= 104), and for
+            // the numerator +0 the sequence returns the IEEE zero of sign(r) itself
+            const float q = wide ? oy : ox;
+            float rr = __builtin_amdgcn_rcpf(r);
+            rr = __builtin_fmaf(__builtin_fmaf(-r, rr, 1.0f), rr, rr);
+            float qq = q * rr;
+            qq = __builtin_fmaf(__builtin_fmaf(-r, qq, q), rr, qq);
+            t = kPiOver4 * __builtin_fmaf(__builtin_fmaf(-r, qq, q), rr, qq);
+        } else {
+            t = kPiOver4 * ((wide ? oy : ox) / r);
+        }
         const float pc = poly_cos(t), ps = poly_sin(t);
         dx = r * (wide ? pc : ps);
         dy = r * (wide ? ps : pc);
@@ -1224,7 +1317,7 @@ void trace_kernel(TraceParams P) {
                     // reference recomputes it with pdf = 1e-4.  (a / pdf) * InvPi is NaN
                     // exactly when a / pdf is, so the condition is decided before dividing.
                     V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                    V3 adp = div3_nan_guard(ad, pdf);
+                    V3 adp = lambert_div<FSQ>(ad, pdf, cw, P.shade_fast);
                     V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
                     beta = beta * nb;
                     // sample_direct_lighting (tracing.py:92-108)
@@ -1287,7 +1380,8 @@ void trace_kernel(TraceParams P) {
                         const float* em = s_mats + 8 * __float_as_int(LN.w);
                         V3 dd = p - p2;
                         float sl = dot(dd, dd);
-                        V3 rad = div3(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl);
+                        V3 rad = nee_div<FSQ>(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl,
+                                                 dot1, dot2, P.shade_fast);
                         pend = beta * rad;
                         d = w;
                         tmax = t_at;
@@ -1800,7 +1894,7 @@ void trace_kernel_pool(TraceParams P) {
                         float cw = dot(n, wi);
                         float dz = cw > 0.0f ? cw : 0.0f;
                         V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                        V3 adp = div3_nan_guard(ad, pdf);
+                        V3 adp = lambert_div<true>(ad, pdf, cw, P.shade_fast);
                         V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
                         beta = beta * nb;
                         int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
@@ -1832,7 +1926,8 @@ void trace_kernel_pool(TraceParams P) {
                                 const float* em = s_mats + 8 * __float_as_int(LN.w);
                                 V3 dd = p - p2;
                                 float sl = dot(dd, dd);
-                                V3 rad = div3(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl);
+                                V3 rad = nee_div<true>(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl,
+                                                         dot1, dot2, P.shade_fast);
                                 pend = beta * rad;
                                 pool[3 * kBlock + tid] = w.x; pool[4 * kBlock + tid] = w.y; pool[5 * kBlock + tid] = w.z;
                                 pool[6 * kBlock + tid] = t_at;

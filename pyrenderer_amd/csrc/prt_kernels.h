@@ -60,6 +60,8 @@ struct TraceParams {
     int cam_clears;
     int lds_stack;            // pool kernel: 16-bit LDS traversal stack entries per lane (>= the BVH4's need)
     int plain;                // 1: no spheres and no metal / dielectric material (the pool kernel's lean build)
+    int shade_fast;           // 1: every material's rho in [2^-40, 2^40] and every face normal's length in
+                              // [0.5, 2] (host-checked): the shading quotients' cheap guards (prt_device.h)
 };
 
 // trace kernel variants (selectable at run time through PRT_FLAG_VARIANT).  All run the
@@ -121,6 +123,8 @@ int trace_blocks_per_cu(int stack, int var, bool stats, size_t smem);
 // mismatches of the fast reciprocal sequence against 1 / b over all 2^32 floats, by class of |b|
 // (8 counters: zero, denormal, < 2^-40, [2^-40, 2^40], (2^40, 2^126], > 2^126, inf, NaN)
 hipError_t launch_rcp_selftest(unsigned long long* d_out, hipStream_t stream);
+// the fast sequences' guards over all 2^32 floats (10 counters, prt_kernels.hip guard_selftest_kernel)
+hipError_t launch_guard_selftest(unsigned long long* d_out, hipStream_t stream);
 // the block-pooled shadow-query kernel (prt_trace_pool.hip): launch / blocks per CU by (stats, waves per EU)
 // the pooled kernel's lean instantiation (no sphere or specular code) runs when P.plain is set
 hipError_t launch_trace_pool(const TraceParams& P, bool stats, int wpe, int grid, size_t smem, hipStream_t stream);

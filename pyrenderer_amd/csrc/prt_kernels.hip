@@ -344,7 +344,52 @@ __global__ void rcp_selftest_kernel(unsigned long long* out) {
         }
     }
 }
+
+// The guards of the fast sequences (prt_selftest_guards): one sweep over all 2^32 floats b counts, for
+// rcp_fast_seq against 1.0f / b and sqrt_fast_seq against sqrtf (both NaN = equal):
+//   0  rcp mismatches the output-class guard accepts (class(r) normal: rcp_exact) — must be 0
+//   1  rcp operands the output-class guard sends to the division
+//   2  rcp mismatches in all
+//   3  rcp mismatches for normal |b| <= 2^126 (round 5's statement) — must be 0
+//   4  sqrt mismatches the guard accepts (b >= 2^-96: sqrt_cr) — must be 0
+//   5  sqrt operands the guard sends to sqrtf
+//   6  sqrt mismatches in all
+//   7  sqrt mismatches for b in [2^-96, FLT_MAX] (round 5's range guard) — must be 0
+//   8  sqrt mismatches for +0 and +normal b < 2^-96
+//   9  sqrt mismatches for denormal b
+__global__ void guard_selftest_kernel(unsigned long long* out) {
+    const uint64_t n = 1ull << 32;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t c[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float b = __uint_as_float((uint32_t)i);
+        auto same = [](float x, float y) { return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y); };
+        const float r = rcp_fast_seq(b);
+        const bool rs = same(r, 1.0f / b);
+        const bool r_ok = rcp_guard_ok(r);
+        c[0] += (!rs && r_ok) ? 1u : 0u;
+        c[1] += r_ok ? 0u : 1u;
+        c[2] += rs ? 0u : 1u;
+        c[3] += (!rs && __builtin_amdgcn_classf(b, kClassNormal) && fabsf(b) <= 0x1p126f) ? 1u : 0u;
+        const float q = sqrt_fast_seq(b);
+        const bool qs = same(q, sqrtf(b));
+        const bool q_ok = sqrt_guard_ok(b);
+        c[4] += (!qs && q_ok) ? 1u : 0u;
+        c[5] += q_ok ? 0u : 1u;
+        c[6] += qs ? 0u : 1u;
+        c[7] += (!qs && b >= 0x1p-96f && b <= 0x1.fffffep127f) ? 1u : 0u;
+        c[8] += (!qs && b >= 0.0f && b < 0x1p-96f && __builtin_amdgcn_classf(b, kClassPosNormal | kClassPosZero)) ? 1u : 0u;
+        c[9] += (!qs && __builtin_amdgcn_classf(b, kClassDenorm)) ? 1u : 0u;
+    }
+    for (int k = 0; k < 10; ++k)
+        if (c[k]) atomicAdd(out + k, (unsigned long long)c[k]);
+}
 }  // namespace
+
+hipError_t launch_guard_selftest(unsigned long long* d_out, hipStream_t stream) {
+    guard_selftest_kernel<<<4096, 256, 0, stream>>>(d_out);
+    return hipGetLastError();
+}
 
 hipError_t launch_rcp_selftest(unsigned long long* d_out, hipStream_t stream) {
     rcp_selftest_kernel<<<4096, 256, 0, stream>>>(d_out);
