@@ -6,7 +6,7 @@ set -e
 SRC=$1; DST=$2
 [ -d $SRC/prof_c2 ] && python tools/pmc_summary.py --dir $SRC/prof_c2 --key cornell_512x512x64spp_d8 > /dev/null
 [ -d $SRC/prof_c4 ] && python tools/pmc_summary.py --dir $SRC/prof_c4 --key cubes_512x512x64spp_d8 > /dev/null
-# configs 1 / 3 / 5 when tools/prof_135.sh ran into the same directory
+# configs 1 / 3 / 5 when the profile stage covered them
 [ -d $SRC/prof_c1 ] && python tools/pmc_summary.py --dir $SRC/prof_c1 --key cornell_128x128x4spp_d4 > /dev/null
 [ -d $SRC/prof_c3 ] && python tools/pmc_summary.py --dir $SRC/prof_c3 --key specular_1024x1024x256spp_d8 > /dev/null
 [ -d $SRC/prof_c5 ] && python tools/pmc_summary.py --dir $SRC/prof_c5 --key cornell_4096x4096x256spp_d8 > /dev/null
