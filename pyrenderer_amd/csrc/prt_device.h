@@ -905,6 +905,11 @@ void trace_kernel(TraceParams P) {
     constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
     constexpr bool MIS = (VAR & 256) != 0;     // MIS direct lighting (sample_direct_lighting2) instead of NEE
     constexpr bool FSQ = SCENE_LDS;            // shading sqrt fast path (sqrt_cr)
+#ifdef PRT_GLOBAL_FASTDIV
+    constexpr bool FDIV = true;
+#else
+    constexpr bool FDIV = FSQ;                 // the shading quotients' cheap guards (lambert_div, nee_div)
+#endif
     extern __shared__ float4 smem[];
     // LDS: the traversal stacks (16-bit entries for LDS-resident scenes), then the scene copy
     using StackT = typename std::conditional<SPILL, SpillStack<STACK>,
@@ -1320,7 +1325,7 @@ void trace_kernel(TraceParams P) {
                     // reference recomputes it with pdf = 1e-4.  (a / pdf) * InvPi is NaN
                     // exactly when a / pdf is, so the condition is decided before dividing.
                     V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                    V3 adp = lambert_div<FSQ>(ad, pdf, cw, P.shade_fast);
+                    V3 adp = lambert_div<FDIV>(ad, pdf, cw, P.shade_fast);
                     V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
                     beta = beta * nb;
                     // sample_direct_lighting (tracing.py:92-108)
@@ -1383,7 +1388,7 @@ void trace_kernel(TraceParams P) {
                         const float* em = s_mats + 8 * __float_as_int(LN.w);
                         V3 dd = p - p2;
                         float sl = dot(dd, dd);
-                        V3 rad = nee_div<FSQ>(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl,
+                        V3 rad = nee_div<FDIV>(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl,
                                                  dot1, dot2, P.shade_fast);
                         pend = beta * rad;
                         d = w;
