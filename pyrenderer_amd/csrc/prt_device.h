@@ -905,11 +905,9 @@ void trace_kernel(TraceParams P) {
     constexpr bool RESUME = (VAR & 128) != 0;  // suspend the traversal tail, resume next iteration
     constexpr bool MIS = (VAR & 256) != 0;     // MIS direct lighting (sample_direct_lighting2) instead of NEE
     constexpr bool FSQ = SCENE_LDS;            // shading sqrt fast path (sqrt_cr)
-#ifdef PRT_GLOBAL_FASTDIV
-    constexpr bool FDIV = true;
-#else
-    constexpr bool FDIV = FSQ;                 // the shading quotients' cheap guards (lambert_div, nee_div)
-#endif
+    // the shading quotients' cheap guards (lambert_div, nee_div): LDS scenes; in the global-scene kernel
+    // (L1-bound) they measured +0.3 % at C4 (profiles/r06/guards/ab_c4_global_fastdiv.jsonl)
+    constexpr bool FDIV = FSQ;
     extern __shared__ float4 smem[];
     // LDS: the traversal stacks (16-bit entries for LDS-resident scenes), then the scene copy
     using StackT = typename std::conditional<SPILL, SpillStack<STACK>,

@@ -9,10 +9,11 @@
 // share a node in groups of `share` (1: 64 distinct lines per load, 64: one line); `active` lanes of
 // each wave load (the others idle, as divergent traversal lanes).  Kernel time per wave-load over the
 // sharing factors tells whether distinct lines, not lanes, set the cost.
-//   hipcc --offload-arch=gfx950 -O3 -o /tmp/l1_lines tools/micro/l1_lines.hip && /tmp/l1_lines
+//   hipcc --offload-arch=gfx950 -O3 -o /tmp/l1_lines tools/micro/l1_lines.hip && /tmp/l1_lines [KiB]
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 constexpr int kIters = 2048;
@@ -37,8 +38,11 @@ __global__ __launch_bounds__(256) void chase(const float4* __restrict__ nodes, u
     if (acc == 12345.0f) out[0] = acc;
 }
 
-int main() {
-    const uint32_t n_nodes = 11u << 20 >> 6;   // 11 MB of 64-B nodes
+int main(int argc, char** argv) {
+    // node array size in KiB (default 11 MiB, config 4's quantised nodes; 16 KiB stays in the vector L1,
+    // 2 MiB in L2)
+    const uint32_t kib = argc > 1 ? (uint32_t)atoi(argv[1]) : 11u << 10;
+    const uint32_t n_nodes = kib << 10 >> 6;
     std::vector<float> host((size_t)n_nodes * 16);
     for (size_t i = 0; i < host.size(); ++i) host[i] = (float)(i % 7) * 1e-3f;
     float4* d_nodes;
@@ -52,7 +56,7 @@ int main() {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    std::printf("{\"cus\": %d, \"iters\": %d, \"rows\": [\n", prop.multiProcessorCount, kIters);
+    std::printf("{\"cus\": %d, \"iters\": %d, \"kib\": %u, \"rows\": [\n", prop.multiProcessorCount, kIters, kib);
     bool first = true;
     for (int active : {64, 32}) {
         for (int share : {1, 2, 4, 8, 16, 64}) {
