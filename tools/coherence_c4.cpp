@@ -132,7 +132,26 @@ struct Model {
 };
 
 struct Stats { double rays = 0, node_trips = 0, node_lanes = 0, node_lines64 = 0, node_lines128 = 0,
-               tri_trips = 0, tri_lanes = 0, tri_lines = 0; };
+               tri_trips = 0, tri_lanes = 0, tri_lines = 0, node_quad_cost = 0; };
+
+// The vector-L1 cost of one wave load by lane quads, as tools/micro/l1_lines.hip measured it on
+// L1/L2-resident nodes (profiles/r06/micro/): a quad whose active lanes all read ONE node costs 0.26 of
+// a quad whose lanes read two or more (lanes sharing nodes in pairs cost as much as all-distinct lanes);
+// a quad without active lanes costs nothing
+double quad_cost(const int32_t* node_of_lane, int n) {
+    double c = 0.0;
+    for (int q = 0; q < n; q += 4) {
+        int32_t first = -1;
+        bool any = false, uniform = true;
+        for (int j = q; j < std::min(n, q + 4); ++j) {
+            if (node_of_lane[j] < 0) continue;
+            if (!any) { first = node_of_lane[j]; any = true; }
+            else if (node_of_lane[j] != first) uniform = false;
+        }
+        c += !any ? 0.0 : uniform ? 0.26 : 1.0;
+    }
+    return c;
+}
 
 // lockstep waves: trip k of a wave holds every lane's k-th element
 void wave(const std::vector<const Visit*>& lanes, Stats& s) {
@@ -140,12 +159,17 @@ void wave(const std::vector<const Visit*>& lanes, Stats& s) {
     size_t kn = 0, kt = 0;
     for (auto* v : lanes) { kn = std::max(kn, v->nodes.size()); kt = std::max(kt, v->tris.size()); }
     std::unordered_set<int64_t> a, b, c;
+    int32_t nl[64];
     for (size_t k = 0; k < kn; ++k) {
         a.clear(); b.clear();
         int act = 0;
-        for (auto* v : lanes)
+        for (size_t j = 0; j < lanes.size(); ++j) {
+            const Visit* v = lanes[j];
+            nl[j] = k < v->nodes.size() ? v->nodes[k] : -1;
             if (k < v->nodes.size()) { ++act; a.insert(v->nodes[k]); b.insert(v->nodes[k] >> 1); }
+        }
         s.node_trips += 1; s.node_lanes += act; s.node_lines64 += (double)a.size(); s.node_lines128 += (double)b.size();
+        s.node_quad_cost += quad_cost(nl, (int)lanes.size());
     }
     for (size_t k = 0; k < kt; ++k) {
         c.clear();
@@ -254,6 +278,7 @@ int main(int argc, char** argv) {
             auto& T = (kind & 1) ? tot_sh[sc] : tot_ext[sc];
             T.rays += s.rays; T.node_trips += s.node_trips; T.node_lanes += s.node_lanes; T.node_lines64 += s.node_lines64;
             T.node_lines128 += s.node_lines128; T.tri_trips += s.tri_trips; T.tri_lanes += s.tri_lanes; T.tri_lines += s.tri_lines;
+            T.node_quad_cost += s.node_quad_cost;
             std::printf(", \"%s\": {\"node_lines_per_ray\": %.3f, \"node_lines_per_trip\": %.2f, \"tri_lines_per_ray\": %.3f}",
                         sc.c_str(), s.node_lines64 / s.rays, s.node_lines64 / std::max(1.0, s.node_trips), s.tri_lines / s.rays);
         }
@@ -298,11 +323,11 @@ int main(int argc, char** argv) {
             std::printf("%s\"%s\": {\"rays\": %.0f, \"node_visits_per_ray\": %.2f, \"node_trips_per_ray\": %.4f, "
                         "\"node_lanes\": %.3f, \"node_lines64_per_ray\": %.3f, \"node_lines128_per_ray\": %.3f, "
                         "\"node_lines64_per_trip\": %.2f, \"tri_tests_per_ray\": %.2f, \"tri_lines_per_ray\": %.3f, "
-                        "\"tri_lines_per_trip\": %.2f}",
+                        "\"tri_lines_per_trip\": %.2f, \"node_quad_cost_per_ray\": %.3f}",
                         fs ? "" : ", ", sc.c_str(), s.rays, s.node_lanes / s.rays, s.node_trips / s.rays,
                         s.node_lanes / (64.0 * s.node_trips), s.node_lines64 / s.rays, s.node_lines128 / s.rays,
                         s.node_lines64 / s.node_trips, s.tri_lanes / s.rays, s.tri_lines / s.rays,
-                        s.tri_lines / std::max(1.0, s.tri_trips));
+                        s.tri_lines / std::max(1.0, s.tri_trips), s.node_quad_cost / s.rays);
             fs = false;
         }
         std::printf("}");
