@@ -16,7 +16,7 @@ import pytest
 from conftest import ROOT
 
 PMC = os.path.join(ROOT, "profiles", "pmc.json")
-FINAL = os.path.join(ROOT, "profiles", "r05", "final")
+FINAL = os.path.join(ROOT, "profiles", "r06", "final")
 # headline workloads: config 2 (bench.py default) on the LDS-resident pooled-shadow kernel, config 4
 # on the global-scene kernel
 KEYS = {"cornell_512x512x64spp_d8": ("prof_c2", 7), "cubes_512x512x64spp_d8": ("prof_c4", 3)}
