@@ -155,27 +155,29 @@ double quad_cost(const int32_t* node_of_lane, int n) {
 
 // lockstep waves: trip k of a wave holds every lane's k-th element
 void wave(const std::vector<const Visit*>& lanes, Stats& s) {
-    s.rays += (double)lanes.size();
+    static const Visit kIdle;   // an idle lane (null entry): no visits, keeps its position in the quads
+    std::vector<const Visit*> L(lanes.size());
+    for (size_t j = 0; j < lanes.size(); ++j) { L[j] = lanes[j] ? lanes[j] : &kIdle; s.rays += lanes[j] ? 1.0 : 0.0; }
     size_t kn = 0, kt = 0;
-    for (auto* v : lanes) { kn = std::max(kn, v->nodes.size()); kt = std::max(kt, v->tris.size()); }
+    for (auto* v : L) { kn = std::max(kn, v->nodes.size()); kt = std::max(kt, v->tris.size()); }
     std::unordered_set<int64_t> a, b, c;
     int32_t nl[64];
     for (size_t k = 0; k < kn; ++k) {
         a.clear(); b.clear();
         int act = 0;
-        for (size_t j = 0; j < lanes.size(); ++j) {
-            const Visit* v = lanes[j];
+        for (size_t j = 0; j < L.size(); ++j) {
+            const Visit* v = L[j];
             nl[j] = k < v->nodes.size() ? v->nodes[k] : -1;
             if (k < v->nodes.size()) { ++act; a.insert(v->nodes[k]); b.insert(v->nodes[k] >> 1); }
         }
         s.node_trips += 1; s.node_lanes += act; s.node_lines64 += (double)a.size(); s.node_lines128 += (double)b.size();
-        s.node_quad_cost += quad_cost(nl, (int)lanes.size());
+        s.node_quad_cost += quad_cost(nl, (int)L.size());
     }
     for (size_t k = 0; k < kt; ++k) {
         c.clear();
         int act = 0;
         // a 48-B record spans one or two 64-B lines
-        for (auto* v : lanes)
+        for (auto* v : L)
             if (k < v->tris.size()) { ++act; c.insert((int64_t)v->tris[k] * 48 / 64); c.insert(((int64_t)v->tris[k] * 48 + 47) / 64); }
         s.tri_trips += 1; s.tri_lanes += act; s.tri_lines += (double)c.size();
     }
@@ -295,20 +297,31 @@ int main(int argc, char** argv) {
                 if ((rays[i].kind >> 3) == 0) queue.push_back(rays[i].pixel);
                 path[rays[i].pixel].push_back(i);
             }
-        Stats s;
-        size_t qn = 0;
-        std::vector<int> lane_px(64, -1), lane_b(64, 0);
-        while (true) {
-            std::vector<const Visit*> lanes;
-            for (int j = 0; j < 64; ++j) {
-                if (lane_px[j] >= 0 && lane_b[j] >= (int)path[lane_px[j]].size()) lane_px[j] = -1;
-                if (lane_px[j] < 0 && qn < queue.size()) { lane_px[j] = queue[qn++]; lane_b[j] = 0; }
-                if (lane_px[j] >= 0) lanes.push_back(&vis[path[lane_px[j]][(size_t)lane_b[j]++]]);
+        // quad: a quad of lanes refills only when all four are idle, with four consecutive pixels
+        for (int quad = 0; quad < 2; ++quad) {
+            Stats s;
+            size_t qn = 0;
+            std::vector<int> lane_px(64, -1), lane_b(64, 0);
+            while (true) {
+                std::vector<const Visit*> lanes(64, nullptr);
+                bool any = false;
+                for (int j = 0; j < 64; ++j)
+                    if (lane_px[j] >= 0 && lane_b[j] >= (int)path[lane_px[j]].size()) lane_px[j] = -1;
+                for (int j = 0; j < 64; ++j) {
+                    if (quad) {
+                        if ((j & 3) == 0 && lane_px[j] < 0 && lane_px[j + 1] < 0 && lane_px[j + 2] < 0 && lane_px[j + 3] < 0)
+                            for (int t = 0; t < 4 && qn < queue.size(); ++t) { lane_px[j + t] = queue[qn++]; lane_b[j + t] = 0; }
+                    } else if (lane_px[j] < 0 && qn < queue.size()) {
+                        lane_px[j] = queue[qn++];
+                        lane_b[j] = 0;
+                    }
+                    if (lane_px[j] >= 0) { lanes[(size_t)j] = &vis[path[lane_px[j]][(size_t)lane_b[j]++]]; any = true; }
+                }
+                if (!any) break;
+                wave(lanes, s);
             }
-            if (lanes.empty()) break;
-            wave(lanes, s);
+            tot_ext[quad ? "quadregen" : "regen"] = s;
         }
-        tot_ext["regen"] = s;
     }
     std::printf("}, \"totals\": {");
     bool fk = true;
@@ -317,7 +330,7 @@ int main(int argc, char** argv) {
         fk = false;
         bool fs = true;
         std::vector<std::string> all = scheds;
-        if (T == &tot_ext) all.insert(all.begin(), "regen");
+        if (T == &tot_ext) all.insert(all.begin(), {"regen", "quadregen"});
         for (const auto& sc : all) {
             const Stats& s = (*T)[sc];
             std::printf("%s\"%s\": {\"rays\": %.0f, \"node_visits_per_ray\": %.2f, \"node_trips_per_ray\": %.4f, "
