@@ -437,7 +437,10 @@ constexpr uint32_t kGuardTrips = 1u << 20;   // leaf batches per query before th
 // occupancy and the spill branch is almost never taken.
 struct LdsStack {
     static constexpr int kSent = kSentinel;
+    static constexpr int kStep = 1;   // sp advances by kStep per entry (LdsStack16A: bytes)
     int* l;
+    __device__ __forceinline__ int origin() const { return 0; }
+    __device__ __forceinline__ int depth(int sp) const { return sp; }
     __device__ __forceinline__ void put(int k, int v) { l[k * kBlock] = v; }
     __device__ __forceinline__ int get(int k) const { return l[k * kBlock]; }
     // entries [0, k] of every lane are in LDS (always)
@@ -447,7 +450,10 @@ struct LdsStack {
 template <int LST>
 struct SpillStack {
     static constexpr int kSent = kSentinel;
+    static constexpr int kStep = 1;
     int* l;
+    __device__ __forceinline__ int origin() const { return 0; }
+    __device__ __forceinline__ int depth(int sp) const { return sp; }
     int* g;
     uint32_t gs;
     __device__ __forceinline__ void put(int k, int v) {
@@ -467,12 +473,45 @@ struct SpillStack {
 // different banks.
 struct LdsStack16 {
     static constexpr int kSent = 0x7FFF;
+    static constexpr int kStep = 1;
     short* l;
+    __device__ __forceinline__ int origin() const { return 0; }
+    __device__ __forceinline__ int depth(int sp) const { return sp; }
     __device__ __forceinline__ void put(int k, int v) { l[k * kBlock] = (short)v; }
     __device__ __forceinline__ int get(int k) const { return (int)l[k * kBlock]; }
     __device__ __forceinline__ bool lds_only(int) const { return true; }
     __device__ __forceinline__ LdsStack16 lds() const { return *this; }
 };
+// LdsStack16 with the stack pointer held as the entry's LDS byte ADDRESS (round 6): a push writes at
+// sp + kStep as an immediate offset of the pointer register and advances it by a select, a pop reads at
+// sp — no per-entry address arithmetic (the index form spends a v_lshl_add on every push and pop:
+// three or four per node visit)
+typedef __attribute__((address_space(3))) short LdsShort;
+struct LdsStack16A {
+    static constexpr int kSent = 0x7FFF;
+    static constexpr int kStep = 2 * kBlock;
+    int base;   // LDS byte address of this lane's entry 0
+    __device__ __forceinline__ void put(int k, int v) { *(LdsShort*)(uintptr_t)(uint32_t)k = (short)v; }
+    __device__ __forceinline__ int get(int k) const { return (int)*(const LdsShort*)(uintptr_t)(uint32_t)k; }
+    __device__ __forceinline__ int origin() const { return base; }
+    __device__ __forceinline__ int depth(int sp) const { return (sp - base) / kStep; }
+    __device__ __forceinline__ bool lds_only(int) const { return true; }
+    __device__ __forceinline__ LdsStack16A lds() const { return *this; }
+};
+// sp advanced by one entry where p holds.  Address form: the 0 / 1 select laundered into a register and
+// shifted by the entry stride (one v_cndmask + one v_lshl_add); as a select of 0 / 512 the stride would
+// need a VGPR of its own (gfx950 reads one scalar operand per VALU instruction besides the mask), which
+// the pooled kernel pays with spills
+template <class S>
+__device__ __forceinline__ int stack_adv(int sp, bool p) {
+    if constexpr (S::kStep == 1) {
+        return sp + (p ? 1 : 0);
+    } else {
+        int b = p ? 1 : 0;
+        asm volatile("" : "+v"(b));
+        return sp + (b << __builtin_ctz(S::kStep));
+    }
+}
 
 // MODE 0: per-lane query kind (`any` may differ between lanes); 1: every lane
 // closest-hit; 2: every lane any-hit (phase-aligned shadow iterations).  Any-hit
@@ -528,8 +567,8 @@ __device__ __forceinline__ int root_for(float tmax) { return tmax == tmax ? 0 : 
 
 template <class S>
 __device__ __forceinline__ void tstate_init(TState& ts, S stk, float tmax) {
-    stk.put(0, S::kSent);
-    ts.cur = root_for<S>(tmax); ts.leaf = 0; ts.sp = 0; ts.best_id = -1; ts.best = tmax;
+    stk.put(stk.origin(), S::kSent);
+    ts.cur = root_for<S>(tmax); ts.leaf = 0; ts.sp = stk.origin(); ts.best_id = -1; ts.best = tmax;
 }
 
 // RES: the wave leaves the traversal loop once fewer than `min_lanes` lanes are still
@@ -656,20 +695,20 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
             // LAST hit child: back to front is 4.6 % faster at C2 than front to back for the
             // shadow rays (they end at the light, and an occluder near it ends the query)
             const bool p3 = h3 & (h0 | h1 | h2), p2 = h2 & (h0 | h1), p1 = h1 & h0;
-            st.put(sp + 1, r3); sp += p3 ? 1 : 0;
-            st.put(sp + 1, r2); sp += p2 ? 1 : 0;
-            st.put(sp + 1, r1); sp += p1 ? 1 : 0;
+            st.put(sp + S::kStep, r3); sp = stack_adv<S>(sp, p3);
+            st.put(sp + S::kStep, r2); sp = stack_adv<S>(sp, p2);
+            st.put(sp + S::kStep, r1); sp = stack_adv<S>(sp, p1);
             const int tp = st.get(sp);
             const bool any_hit = h0 | h1 | h2 | h3;
             cur = h0 ? r0 : (h1 ? r1 : (h2 ? r2 : (h3 ? r3 : tp)));
-            sp -= any_hit ? 0 : 1;
+            sp -= any_hit ? 0 : S::kStep;
         } else if (MODE == 2) {
-            st.put(sp + 1, r0); sp += h0 ? 1 : 0;
-            st.put(sp + 1, r1); sp += h1 ? 1 : 0;
-            st.put(sp + 1, r2); sp += h2 ? 1 : 0;
+            st.put(sp + S::kStep, r0); sp = stack_adv<S>(sp, h0);
+            st.put(sp + S::kStep, r1); sp = stack_adv<S>(sp, h1);
+            st.put(sp + S::kStep, r2); sp = stack_adv<S>(sp, h2);
             int top = st.get(sp);
             cur = h3 ? r3 : top;
-            sp -= h3 ? 0 : 1;
+            sp -= h3 ? 0 : S::kStep;
         } else {
             // nearest hit child first by a 3-comparator tournament on the entry distances
             // (misses count as +inf, a hit's distance is finite); the three others are pushed
@@ -690,16 +729,16 @@ __device__ __forceinline__ void visit_node4(const float4* __restrict__ nodes, in
             const bool m = c < a;
             const int rn = m ? rc : ra, rl = m ? ra : rc;
             const float xn = m ? c : a, xl = m ? a : c;
-            st.put(sp + 1, rb); sp += xb < INFINITY ? 1 : 0;
-            st.put(sp + 1, rd); sp += xd < INFINITY ? 1 : 0;
-            st.put(sp + 1, rl); sp += xl < INFINITY ? 1 : 0;
+            st.put(sp + S::kStep, rb); sp += xb < INFINITY ? S::kStep : 0;
+            st.put(sp + S::kStep, rd); sp += xd < INFINITY ? S::kStep : 0;
+            st.put(sp + S::kStep, rl); sp += xl < INFINITY ? S::kStep : 0;
             const int tp = st.get(sp);
             const bool any_hit = xn < INFINITY;
             cur = any_hit ? rn : tp;
-            sp -= any_hit ? 0 : 1;
+            sp -= any_hit ? 0 : S::kStep;
         }
     };
-    if (stk.lds_only(sp + 3)) step(stk.lds());
+    if (stk.lds_only(sp + 3 * S::kStep)) step(stk.lds());
     else step(stk);
 }
 
@@ -729,11 +768,11 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
         while (cur >= 0 && cur != S::kSent) {
             visit_node4<STATS, MODE, S, QN, OCT>(nodes, cur, sp, stk, inv, oi, sx, sy, sz, tmin, best, cn, any);
             if (STATS) wave_tick(cn.wi, cn.li);
-            if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(sp + 1));
+            if (STATS) cn.max_sp = max(cn.max_sp, (uint32_t)(stk.depth(sp) + 1));
             if (cur < 0 && leaf >= 0) {   // postpone the leaf, keep descending
                 leaf = cur;
                 cur = stk.get(sp);
-                --sp;
+                sp -= S::kStep;
             }
             // leave for the leaf phase once at most `leaf_break` of the lanes still
             // descending have no postponed leaf (0: all of them hold one)
@@ -774,7 +813,7 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
             leaf = cur;
             if (cur < 0) {
                 cur = stk.get(sp);
-                --sp;
+                sp -= S::kStep;
             }
             // back to the inner phase once at most `leaf_exit` lanes still hold a leaf
             // (they keep it postponed); 0: drain every lane's chain of leaves first
@@ -911,12 +950,12 @@ void trace_kernel(TraceParams P) {
     extern __shared__ float4 smem[];
     // LDS: the traversal stacks (16-bit entries for LDS-resident scenes), then the scene copy
     using StackT = typename std::conditional<SPILL, SpillStack<STACK>,
-                                             typename std::conditional<SCENE_LDS, LdsStack16, LdsStack>::type>::type;
+                                             typename std::conditional<SCENE_LDS, LdsStack16A, LdsStack>::type>::type;
     constexpr int kStackF4 = STACK * kBlock * (SCENE_LDS ? 2 : 4) / 16;
     StackT stk;
     if constexpr (SCENE_LDS) {
         const int t = threadIdx.x;
-        stk.l = reinterpret_cast<short*>(smem) + (t & ~63) + 2 * (t & 31) + ((t >> 5) & 1);
+        stk.base = (int)(uintptr_t)(LdsShort*)(reinterpret_cast<short*>(smem) + (t & ~63) + 2 * (t & 31) + ((t >> 5) & 1));
     } else {
         stk.l = reinterpret_cast<int*>(smem) + threadIdx.x;
     }
@@ -1623,8 +1662,12 @@ void trace_kernel_pool(TraceParams P) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int stack_f4 = P.lds_stack * kBlock * 2 / 16;
-    LdsStack16 stk;
-    stk.l = reinterpret_cast<short*>(smem) + (tid & ~63) + 2 * (tid & 31) + ((tid >> 5) & 1);
+    // LdsStack16's entry layout with the stack pointer as an LDS address (round 6: C2 -0.2 %, C3 -0.5 %
+    // per launch against the index form, profiles/r06/stack/)
+    LdsStack16A stk;
+    stk.base = (int)(uintptr_t)(LdsShort*)(reinterpret_cast<short*>(smem) + (tid & ~63) + 2 * (tid & 31) +
+                                           ((tid >> 5) & 1));
+    using Stk = decltype(stk);
     float* pool = reinterpret_cast<float*>(smem + stack_f4);   // [7][256]
     uint8_t* queue = reinterpret_cast<uint8_t*>(smem + stack_f4 + kPoolF4);
     uint32_t* ctl = reinterpret_cast<uint32_t*>(smem + stack_f4 + kPoolF4 + kQueueF4);
@@ -1770,7 +1813,7 @@ void trace_kernel_pool(TraceParams P) {
             if (STATS && lane == __builtin_amdgcn_readfirstlane(lane)) n_e++;
             if (trav) {
                 if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
-                hit = traverse_ww4<STATS, 1, LdsStack16, false, false, true>(
+                hit = traverse_ww4<STATS, 1, Stk, false, false, true>(
                     g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
                 if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
@@ -2016,7 +2059,7 @@ void trace_kernel_pool(TraceParams P) {
                 int hid = -1;
                 float ht = 0.0f;
                 if (STATS) cn.q0 = cn.nodes;
-                bool hit = traverse_ww4<STATS, 2, LdsStack16, false, false, true>(
+                bool hit = traverse_ww4<STATS, 2, Stk, false, false, true>(
                     g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
                     exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
                 if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
