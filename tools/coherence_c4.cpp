@@ -297,8 +297,10 @@ int main(int argc, char** argv) {
                 if ((rays[i].kind >> 3) == 0) queue.push_back(rays[i].pixel);
                 path[rays[i].pixel].push_back(i);
             }
-        // quad: a quad of lanes refills only when all four are idle, with four consecutive pixels
-        for (int quad = 0; quad < 2; ++quad) {
+        // quad 1: a quad of lanes refills only when all four are idle, with four consecutive pixels;
+        // quad 2: per-lane refills, then the wave's 64 rays permuted across its lanes by origin Morton
+        // code before the traversal (an in-wave sort: bitonic over 64 keys + one ray permutation)
+        for (int quad = 0; quad < 8; ++quad) {
             Stats s;
             size_t qn = 0;
             std::vector<int> lane_px(64, -1), lane_b(64, 0);
@@ -308,7 +310,7 @@ int main(int argc, char** argv) {
                 for (int j = 0; j < 64; ++j)
                     if (lane_px[j] >= 0 && lane_b[j] >= (int)path[lane_px[j]].size()) lane_px[j] = -1;
                 for (int j = 0; j < 64; ++j) {
-                    if (quad) {
+                    if (quad == 1) {
                         if ((j & 3) == 0 && lane_px[j] < 0 && lane_px[j + 1] < 0 && lane_px[j + 2] < 0 && lane_px[j + 3] < 0)
                             for (int t = 0; t < 4 && qn < queue.size(); ++t) { lane_px[j + t] = queue[qn++]; lane_b[j + t] = 0; }
                     } else if (lane_px[j] < 0 && qn < queue.size()) {
@@ -318,9 +320,23 @@ int main(int argc, char** argv) {
                     if (lane_px[j] >= 0) { lanes[(size_t)j] = &vis[path[lane_px[j]][(size_t)lane_b[j]++]]; any = true; }
                 }
                 if (!any) break;
+                if (quad == 3) {   // compaction only: active lanes first, in lane order
+                    std::stable_partition(lanes.begin(), lanes.end(), [](const Visit* v) { return v != nullptr; });
+                }
+                if (quad == 2 || quad >= 4) {
+                    // quad 4..7: coarse keys, Morton code of a 2 / 4 / 8 / 256-cell grid per axis
+                    const double n = quad == 4 ? 2.0 : quad == 5 ? 4.0 : quad == 6 ? 8.0 : quad == 7 ? 256.0 : 1024.0;
+                    std::vector<std::pair<uint64_t, const Visit*>> kv;
+                    for (int j = 0; j < 64; ++j)
+                        kv.push_back({lanes[(size_t)j] ? cell(rays[(size_t)(lanes[(size_t)j] - vis.data())], n) : ~0ull, lanes[(size_t)j]});
+                    std::stable_sort(kv.begin(), kv.end(), [](auto& a, auto& b) { return a.first < b.first; });
+                    for (int j = 0; j < 64; ++j) lanes[(size_t)j] = kv[(size_t)j].second;
+                }
                 wave(lanes, s);
             }
-            tot_ext[quad ? "quadregen" : "regen"] = s;
+            static const char* names[8] = {"regen", "quadregen", "regen_wavesort", "regen_compact", "wavesort_2",
+                                           "wavesort_4", "wavesort_8", "wavesort_256"};
+            tot_ext[names[quad]] = s;
         }
     }
     std::printf("}, \"totals\": {");
@@ -330,7 +346,9 @@ int main(int argc, char** argv) {
         fk = false;
         bool fs = true;
         std::vector<std::string> all = scheds;
-        if (T == &tot_ext) all.insert(all.begin(), {"regen", "quadregen"});
+        if (T == &tot_ext)
+            all.insert(all.begin(), {"regen", "quadregen", "regen_wavesort", "regen_compact", "wavesort_2", "wavesort_4",
+                                     "wavesort_8", "wavesort_256"});
         for (const auto& sc : all) {
             const Stats& s = (*T)[sc];
             std::printf("%s\"%s\": {\"rays\": %.0f, \"node_visits_per_ray\": %.2f, \"node_trips_per_ray\": %.4f, "
