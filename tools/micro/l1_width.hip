@@ -16,6 +16,46 @@
 
 constexpr int kIters = 2048;
 
+// quad-cooperative read: the four lanes of a quad read the four 16-B chunks of ONE node (one dwordx4
+// instruction per node and quad; MODE 0), or all four lanes read the same chunk (MODE 1, the
+// uniform-quad case of l1_lines.hip), or each lane its own node's chunk (MODE 2, scattered)
+template <int MODE>
+__global__ __launch_bounds__(256) void chase_quad(const uint32_t* __restrict__ nodes, uint32_t n_nodes, uint32_t seed,
+                                                  float* out) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t q = MODE == 2 ? tid : tid >> 2, j = tid & 3u;
+    uint32_t h = (q * 0x9E3779B9u) ^ seed;
+    uint32_t acc = 0;
+    for (int i = 0; i < kIters; ++i) {
+        h = h * 747796405u + 2891336453u;
+        const uint32_t idx = (h >> 8) % n_nodes;
+        const uint32_t* p = nodes + (size_t)idx * 16 + (MODE == 1 ? 0u : 4u * j);
+        const uint4 v = *reinterpret_cast<const uint4*>(p);
+        acc += v.x ^ v.y ^ v.z ^ v.w;
+        h ^= acc & 1u;
+    }
+    if (acc == 0x12345u) out[0] = (float)acc;
+}
+
+template <int MODE>
+void run_quad(const uint32_t* d_nodes, uint32_t n_nodes, int grid, float* d_out, int cus, bool& first) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    chase_quad<MODE><<<grid, 256>>>(d_nodes, n_nodes, 1u, d_out);
+    (void)hipEventRecord(e0);
+    for (int r = 0; r < 3; ++r) chase_quad<MODE><<<grid, 256>>>(d_nodes, n_nodes, 2u + r, d_out);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const double wave_insts = 3.0 * grid * 4 * kIters;
+    static const char* names[3] = {"quad reads one node's four chunks", "quad reads one chunk", "lanes read own nodes"};
+    std::printf("%s {\"quad_mode\": \"%s\", \"ms\": %.3f, \"ns_per_wave_inst_per_cu\": %.3f}", first ? "" : ",\n",
+                names[MODE], ms / 3.0, ms * 1e6 / wave_insts * cus);
+    first = false;
+}
+
 template <int W, int N>
 __global__ __launch_bounds__(256) void chase(const uint32_t* __restrict__ nodes, uint32_t n_nodes, uint32_t seed,
                                              float* out) {
@@ -91,6 +131,9 @@ int main(int argc, char** argv) {
     run<12, 4>(d_nodes, n_nodes, grid, d_out, prop.multiProcessorCount, first);
     run<8, 4>(d_nodes, n_nodes, grid, d_out, prop.multiProcessorCount, first);
     run<4, 4>(d_nodes, n_nodes, grid, d_out, prop.multiProcessorCount, first);
+    run_quad<0>(d_nodes, n_nodes, grid, d_out, prop.multiProcessorCount, first);
+    run_quad<1>(d_nodes, n_nodes, grid, d_out, prop.multiProcessorCount, first);
+    run_quad<2>(d_nodes, n_nodes, grid, d_out, prop.multiProcessorCount, first);
     std::printf("\n]}\n");
     hipFree(d_nodes);
     hipFree(d_out);
