@@ -32,12 +32,18 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default="/tmp/c4_rays.f32")
+    ap.add_argument("--scene", default="cubes", choices=("cubes", "cornell"),
+                    help="config 4's instanced cubes (default) or the Cornell box of configs 1, 2 and 5")
     a = ap.parse_args()
     from oracle import oracle as O
     from pyrenderer_amd import scenes
     from pyrenderer_amd._native import Bvh
     from pyrenderer_amd.flatten import flatten_scene
-    scene, camera = scenes.instanced_cubes()
+    if a.scene == "cornell":
+        from pyrenderer_amd.io_utils.read_tungsten import read_file
+        scene, camera = read_file(scenes.CORNELL)
+    else:
+        scene, camera = scenes.instanced_cubes()
     flat = flatten_scene(scene)
     flat.tri_v.astype(np.float32).tofile(os.path.splitext(a.out)[0] + "_soup.f32")
     osc = O.OracleScene.from_flat(flat)
