@@ -841,7 +841,26 @@ __device__ __forceinline__ bool traverse_ww4(const float4* __restrict__ nodes, c
 // tile origin (x0 << 16 | y0).  Uniform inputs are laundered through SGPR asm so
 // the compiler cannot hoist their VALU-derived values out of the persistent loop
 // (they would pin VGPRs).
-__device__ __forceinline__ void pixel_of(const TraceParams& P, uint32_t item, uint32_t chunk_s, uint32_t xy0, int& x,
+// The kernel's TraceParams in the kernarg segment, through a pointer the compiler cannot follow: every
+// field read through it is a scalar load (constant cache) at its use instead of a value held in an
+// SGPR across the persistent loop
+typedef const __attribute__((address_space(4))) TraceParams KParams;
+__device__ __forceinline__ KParams& kernarg() {
+    // the kernel's only argument sits at the start of the kernarg segment
+    KParams* k = (KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return *k;
+}
+// trace_kernel: the LDS-scene variants re-read their launch parameters (C1 one-frame launches -13 %,
+// C2 -1.5 % against held values spilled into VGPR lanes); the global-scene variant keeps them (C4 +0.8 %
+// with re-reads, profiles/r06/kernarg/)
+template <bool RELOAD>
+__device__ __forceinline__ auto& params(const TraceParams& P) {
+    if constexpr (RELOAD) return kernarg();
+    else return P;
+}
+template <class PT>
+__device__ __forceinline__ void pixel_of(const PT& P, uint32_t item, uint32_t chunk_s, uint32_t xy0, int& x,
                                          int& y) {
     int log_tw = P.log_tw, log_tpx = P.log_tpx;
     asm volatile("" : "+s"(log_tw), "+s"(log_tpx));
@@ -1081,6 +1100,8 @@ void trace_kernel(TraceParams P) {
     // Lanes whose query kind does not match the wave's phase sit the iteration out.
     bool last_shadow = false;
     while (true) {
+        // LDS scenes: launch parameters re-read through the kernarg pointer each iteration (see params)
+        auto& Q = params<SCENE_LDS>(P);
         if (STATS) { t_a = __builtin_amdgcn_s_memtime(); t_it = t_a; }
         bool do_shadow = false;
         if (PHASE) {
@@ -1096,9 +1117,9 @@ void trace_kernel(TraceParams P) {
             uint32_t avail = q_end - q_next;
             if (avail == 0 && !exhausted) {
                 uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(P.work, (uint32_t)kChunk);
+                if (lane == 0) base = atomicAdd(Q.work, (uint32_t)kChunk);
                 base = __builtin_amdgcn_readfirstlane(base);
-                if ((uint64_t)base >= P.n_items) {
+                if ((uint64_t)base >= Q.n_items) {
                     exhausted = true;
                 } else {
                     if constexpr (!SCENE_LDS) {
@@ -1109,23 +1130,23 @@ void trace_kernel(TraceParams P) {
                         // 18.12 -> 17.51 ms).  LDS scenes keep sample-major chunks, whose staged
                         // rays and radiance are read and written in address order (pixel-major
                         // there strides 4 MB per chunk: C2 4.23 -> 4.32 ms; profiles/r02/s5/ab_pm/)
-                        const uint32_t n_samp = (uint32_t)(P.n_items / (uint64_t)P.n_slots);
+                        const uint32_t n_samp = (uint32_t)(Q.n_items / (uint64_t)Q.n_slots);
                         const uint32_t c = base >> 6;
                         const uint32_t g = c / n_samp;
-                        base = (c - g * n_samp) * (uint32_t)P.n_slots + (g << 6);
+                        base = (c - g * n_samp) * (uint32_t)Q.n_slots + (g << 6);
                         base = __builtin_amdgcn_readfirstlane(base);
                     }
                     q_next = base;
-                    q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
-                    if (P.wave_clock && lane == 0)
-                        P.wave_clock[3 * ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) + 2] += q_end - q_next;
+                    q_end = (uint32_t)min((uint64_t)base + kChunk, Q.n_items);
+                    if (Q.wave_clock && lane == 0)
+                        Q.wave_clock[3 * ((size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) + 2] += q_end - q_next;
                     // n_slots is a multiple of 64 (tile sizes are powers of two >= 64 px),
                     // so a chunk never straddles two samples: one scalar division per chunk
-                    chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
+                    chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)Q.n_slots);
                     // tiles hold >= 64 pixels (powers of two), so the chunk lies in one tile
-                    uint32_t tk = (base - chunk_s * (uint32_t)P.n_slots) >> P.log_tpx;
+                    uint32_t tk = (base - chunk_s * (uint32_t)Q.n_slots) >> Q.log_tpx;
                     // uniform index: a scalar load through the constant address space
-                    chunk_xy0 = ((const __attribute__((address_space(4))) uint32_t*)(uintptr_t)P.tile_xy)[tk];
+                    chunk_xy0 = ((const __attribute__((address_space(4))) uint32_t*)(uintptr_t)Q.tile_xy)[tk];
                 }
                 avail = q_end - q_next;
             }
@@ -1138,28 +1159,28 @@ void trace_kernel(TraceParams P) {
                 // start a new sample: main_taichi.py:89-95
                 L = v3(0, 0, 0);
                 int x, y;
-                pixel_of(P, (uint32_t)item, chunk_s, chunk_xy0, x, y);
-                int W = P.W, H = P.H;
+                pixel_of(Q, (uint32_t)item, chunk_s, chunk_xy0, x, y);
+                int W = Q.W, H = Q.H;
                 asm volatile("" : "+s"(W), "+s"(H));
                 bool ok = x < W && y < H;
                 if (ok) {
                     // primary rays from camera_kernel (or prt_trace_rays' caller rays): no camera code
                     // in the persistent loop, whose uniform operands would spill SGPRs
-                    float4 r = P.rays[item];
+                    float4 r = Q.rays[item];
                     d = v3(r.x, r.y, r.z);
                     st = __float_as_uint(r.w);
-                    if (P.ray_o) {
+                    if (Q.ray_o) {
                         // per-ray origins: prt_trace_rays' caller rays, thin-lens / projective cameras
-                        const float4 ro = P.ray_o[item];
+                        const float4 ro = Q.ray_o[item];
                         o = v3(ro.x, ro.y, ro.z);
                     } else {
-                        float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
+                        float o0 = Q.cam_o[0], o1 = Q.cam_o[1], o2 = Q.cam_o[2];
                         asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
                         o = v3(o0, o1, o2);
                     }
                 }
                 if (!ok) {
-                    float* out = P.out + (size_t)item * 3;
+                    float* out = Q.out + (size_t)item * 3;
                     out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
                     item = -2;  // served, nothing to trace this iteration
                 } else {
@@ -1203,39 +1224,39 @@ void trace_kernel(TraceParams P) {
         }
         // the leaf-phase entry / exit thresholds (counts of lanes) are tuned for full waves; in
         // the drain, with few lanes left, they would switch phase after every trip
-        const int lb = exhausted ? 0 : P.leaf_break, le = exhausted ? 0 : P.leaf_exit;
-        const uint32_t glim = P.guard_trips;
+        const int lb = exhausted ? 0 : Q.leaf_break, le = exhausted ? 0 : Q.leaf_exit;
+        const uint32_t glim = Q.guard_trips;
         if (STATS && !pending) cn.q0 = cn.nodes;   // node visits at the start of this query
         if (RESUME) {
             if (!pending) tstate_init(tst, stk, tmax);
             // suspending a query only pays while idle lanes can be refilled: once the work
             // queue is exhausted (the launch's drain) the wave keeps traversing instead of
             // going round the loop once per inner/leaf phase
-            const int res_min = exhausted ? 0 : P.resume_min;
+            const int res_min = exhausted ? 0 : Q.resume_min;
             bool done;
             if (PHASE && do_shadow)
                 done = traverse_ww4<STATS, 2, StackT, QNODE, true, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
-                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
+                                                                  ht, cn, &tst, res_min, Q.fault, lb, le, glim);
             else if (PHASE)
                 done = traverse_ww4<STATS, 1, StackT, QNODE, true, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
-                                                                  ht, cn, &tst, res_min, P.fault, lb, le, glim);
+                                                                  ht, cn, &tst, res_min, Q.fault, lb, le, glim);
             else
                 done = traverse_ww4<STATS, 0, StackT, QNODE, true, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax,
                                                                   qtype == Q_SHADOW, stk, hid, ht, cn, &tst, res_min,
-                                                                  P.fault, lb, le, glim);
+                                                                  Q.fault, lb, le, glim);
             pending = !done;
             if (pending) continue;   // resume next iteration; no shading yet
             hit = hid >= 0;
         } else if (PHASE) {
             if (do_shadow)
                 hit = traverse_ww4<STATS, 2, StackT, QNODE, false, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, true, stk, hid,
-                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
+                                                                  ht, cn, nullptr, 0, Q.fault, lb, le, glim);
             else
                 hit = traverse_ww4<STATS, 1, StackT, QNODE, false, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, false, stk, hid,
-                                                                  ht, cn, nullptr, 0, P.fault, lb, le, glim);
+                                                                  ht, cn, nullptr, 0, Q.fault, lb, le, glim);
         } else {
             hit = traverse_ww4<STATS, 0, StackT, QNODE, false, SCENE_LDS>(g_nodes, g_tris, o, d, kTMin, tmax, qtype == Q_SHADOW,
-                                                              stk, hid, ht, cn, nullptr, 0, P.fault, lb, le, glim);
+                                                              stk, hid, ht, cn, nullptr, 0, Q.fault, lb, le, glim);
         }
 
         if (STATS) {
@@ -1243,23 +1264,23 @@ void trace_kernel(TraceParams P) {
             cn.max_q = max(cn.max_q, qn);   // most node visits of one query
             // outlier log (diag words 24..151): the first 16 queries with > 1000 node visits
             if (qn > 1000) {
-                const unsigned long long k = atomicAdd(P.stats + 23, 1ull);
+                const unsigned long long k = atomicAdd(Q.stats + 23, 1ull);
                 if (k < 16) {
-                    unsigned long long* r = P.stats + 24 + 8 * k;
+                    unsigned long long* r = Q.stats + 24 + 8 * k;
                     r[0] = __float_as_uint(o.x); r[1] = __float_as_uint(o.y); r[2] = __float_as_uint(o.z);
                     r[3] = __float_as_uint(d.x); r[4] = __float_as_uint(d.y); r[5] = __float_as_uint(d.z);
                     r[6] = __float_as_uint(tmax); r[7] = ((unsigned long long)qtype << 32) | qn;
                 }
             }
         }
-        if (P.n_sph > 0 && !(qtype == Q_SHADOW && hit)) {
+        if (Q.n_sph > 0 && !(qtype == Q_SHADOW && hit)) {
             // analytic spheres after the triangles (ids n_tri + k), same rule as the oracle
             float best = hit ? ht : tmax;
-            for (int k = 0; k < P.n_sph; ++k) {
+            for (int k = 0; k < Q.n_sph; ++k) {
                 float root;
-                if (sphere_hit(P.sph[k], o, d, kTMin, best, root)) {
+                if (sphere_hit(Q.sph[k], o, d, kTMin, best, root)) {
                     best = root;
-                    hid = P.n_tri + k;
+                    hid = Q.n_tri + k;
                     hit = true;
                     if (qtype == Q_SHADOW) break;
                 }
@@ -1290,15 +1311,15 @@ void trace_kernel(TraceParams P) {
                 V3 p = o + d * ht;                                         // ray.at
                 V3 ng;
                 int mid;
-                if (hid < P.n_tri) {
+                if (hid < Q.n_tri) {
                     float4 nm = s_nm[hid];
                     ng = xyz(nm);
                     mid = __float_as_int(nm.w);
                 } else {                                                   // sphere: (p - c) / r
                     asm volatile("");   // keep the divisions in this branch (no if-conversion)
-                    float4 sc = P.sph[hid - P.n_tri];
+                    float4 sc = Q.sph[hid - Q.n_tri];
                     ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
-                    mid = P.sph_mat[hid - P.n_tri];
+                    mid = Q.sph_mat[hid - Q.n_tri];
                 }
                 const float* m = s_mats + 8 * mid;
                 const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;   // shapes.py:101-102
@@ -1331,12 +1352,12 @@ void trace_kernel(TraceParams P) {
                         o = p;
                         d = normalize(out);
                         ++bounce;
-                        if (bounce >= P.depth) finished = true;
+                        if (bounce >= Q.depth) finished = true;
                     }
                 } else if (m[3] != 0.0f) {                                 // tracing.py:129-139
                     float d1 = dot(neg(d), n);
                     if (d1 > 0.0f) {
-                        V3 lc = v3(P.dl_r, P.dl_g, P.dl_b);
+                        V3 lc = v3(Q.dl_r, Q.dl_g, Q.dl_b);
                         L = bounce == 0 ? L + lc * beta : L + (lc * beta) * d1;
                     }
                     finished = true;
@@ -1347,8 +1368,8 @@ void trace_kernel(TraceParams P) {
                     float u0 = rng_next(st);
                     float u1 = rng_next(st);
                     V3 l = cosine_hemisphere<FSQ>(u0, u1);
-                    const float4* fr = s_fr + ((size_t)(hid < P.n_tri ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
-                    if (hid < P.n_tri) {
+                    const float4* fr = s_fr + ((size_t)(hid < Q.n_tri ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
+                    if (hid < Q.n_tri) {
                         float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
                         wi = normalize<FSQ>(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
                     } else {
@@ -1362,11 +1383,11 @@ void trace_kernel(TraceParams P) {
                     // reference recomputes it with pdf = 1e-4.  (a / pdf) * InvPi is NaN
                     // exactly when a / pdf is, so the condition is decided before dividing.
                     V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                    V3 adp = lambert_div<FDIV>(ad, pdf, cw, P.shade_fast);
+                    V3 adp = lambert_div<FDIV>(ad, pdf, cw, Q.shade_fast);
                     V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
                     beta = beta * nb;
                     // sample_direct_lighting (tracing.py:92-108)
-                    int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
+                    int li = Q.n_light > 1 ? rng_int(st, 0, Q.n_light - 1) : 0;
                     int lo = s_loff[li];
                     int f = rng_int(st, 0, s_loff[li + 1] - lo - 1);
                     float su = sqrt_cr<FSQ>(rng_next(st));
@@ -1387,7 +1408,7 @@ void trace_kernel(TraceParams P) {
                         float b0 = rng_next(st);
                         float b1 = rng_next(st);
                         V3 bl = cosine_hemisphere<FSQ>(b0, b1);
-                        if (hid < P.n_tri) {
+                        if (hid < Q.n_tri) {
                             float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
                             mis_bd = normalize<FSQ>(xyz(f0) * bl.x + xyz(f1) * bl.y + xyz(f2) * bl.z);
                         } else {
@@ -1408,7 +1429,7 @@ void trace_kernel(TraceParams P) {
                         } else {
                             L = L + beta * pend;
                             ++bounce;
-                            if (bounce >= P.depth) finished = true;
+                            if (bounce >= Q.depth) finished = true;
                             d = wi;
                             tmax = kTMax;
                         }
@@ -1426,7 +1447,7 @@ void trace_kernel(TraceParams P) {
                         V3 dd = p - p2;
                         float sl = dot(dd, dd);
                         V3 rad = nee_div<FDIV>(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl,
-                                                 dot1, dot2, P.shade_fast);
+                                                 dot1, dot2, Q.shade_fast);
                         pend = beta * rad;
                         d = w;
                         tmax = t_at;
@@ -1434,7 +1455,7 @@ void trace_kernel(TraceParams P) {
                     } else {
                         // no NEE term possible: go straight to the next bounce
                         ++bounce;
-                        if (bounce >= P.depth) finished = true;
+                        if (bounce >= Q.depth) finished = true;
                         d = wi;
                         tmax = kTMax;
                     }
@@ -1444,7 +1465,7 @@ void trace_kernel(TraceParams P) {
         } else if (MIS && qtype == Q_MISL) {
             // light strategy: visible when the closest hit is an emitter
             if (hit) {
-                const int mid = hid < P.n_tri ? __float_as_int(s_nm[hid].w) : P.sph_mat[hid - P.n_tri];
+                const int mid = hid < Q.n_tri ? __float_as_int(s_nm[hid].w) : Q.sph_mat[hid - Q.n_tri];
                 if (s_mats[8 * mid + 3] > 0.0f) {
                     float lp = area_light_pdf(ht, d, mis_n2);
                     float bp = dot_or_zero(mis_n, d) / kPiF;
@@ -1461,7 +1482,7 @@ void trace_kernel(TraceParams P) {
             } else {
                 L = L + beta * pend;
                 ++bounce;
-                if (bounce >= P.depth) finished = true;
+                if (bounce >= Q.depth) finished = true;
                 d = wi;
                 tmax = kTMax;
                 qtype = Q_EXT;
@@ -1469,7 +1490,7 @@ void trace_kernel(TraceParams P) {
         } else if (MIS && qtype == Q_MISB) {
             // BRDF strategy
             if (hit) {
-                const int mid = hid < P.n_tri ? __float_as_int(s_nm[hid].w) : P.sph_mat[hid - P.n_tri];
+                const int mid = hid < Q.n_tri ? __float_as_int(s_nm[hid].w) : Q.sph_mat[hid - Q.n_tri];
                 if (s_mats[8 * mid + 3] > 0.0f) {
                     float lp = area_light_pdf(ht, d, mis_n2);
                     if (lp > 0.0f) {
@@ -1482,20 +1503,20 @@ void trace_kernel(TraceParams P) {
             }
             L = L + beta * pend;
             ++bounce;
-            if (bounce >= P.depth) finished = true;
+            if (bounce >= Q.depth) finished = true;
             d = wi;
             tmax = kTMax;
             qtype = Q_EXT;
         } else {
             if (!hit) L = L + pend;
             ++bounce;
-            if (bounce >= P.depth) finished = true;
+            if (bounce >= Q.depth) finished = true;
             d = wi;           // o is still the hit point p
             tmax = kTMax;
             qtype = Q_EXT;
         }
         if (finished) {
-            float* out = P.out + (size_t)item * 3;
+            float* out = Q.out + (size_t)item * 3;
             out[0] = L.x; out[1] = L.y; out[2] = L.z;
             // failure detection (STATS): samples whose radiance is NaN or infinite
             if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
@@ -1734,23 +1755,23 @@ void trace_kernel_pool(TraceParams P) {
 #define PRT_CLOCK(k) do {} while (0)
 #endif
     // work-queue refill of the wave's idle lanes (path regeneration, trace_kernel's refill)
-    auto refill = [&]() {
+    auto refill = [&](KParams& Q) {
             bool me_idle = item < 0;
             uint64_t idle = __ballot(me_idle);
             for (int round = 0; round < 2 && idle; ++round) {
                 uint32_t avail = q_end - q_next;
                 if (avail == 0 && !exhausted) {
                     uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(P.work, (uint32_t)kChunk);
+                    if (lane == 0) base = atomicAdd(Q.work, (uint32_t)kChunk);
                     base = __builtin_amdgcn_readfirstlane(base);
-                    if ((uint64_t)base >= P.n_items) {
+                    if ((uint64_t)base >= Q.n_items) {
                         exhausted = true;
                     } else {
                         q_next = base;
-                        q_end = (uint32_t)min((uint64_t)base + kChunk, P.n_items);
-                        chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)P.n_slots);
-                        uint32_t tk = (base - chunk_s * (uint32_t)P.n_slots) >> P.log_tpx;
-                        chunk_xy0 = ((const __attribute__((address_space(4))) uint32_t*)(uintptr_t)P.tile_xy)[tk];
+                        q_end = (uint32_t)min((uint64_t)base + kChunk, Q.n_items);
+                        chunk_s = __builtin_amdgcn_readfirstlane(base / (uint32_t)Q.n_slots);
+                        uint32_t tk = (base - chunk_s * (uint32_t)Q.n_slots) >> Q.log_tpx;
+                        chunk_xy0 = ((const __attribute__((address_space(4))) uint32_t*)(uintptr_t)Q.tile_xy)[tk];
                     }
                     avail = q_end - q_next;
                 }
@@ -1762,27 +1783,27 @@ void trace_kernel_pool(TraceParams P) {
                     item = (int)(q_next + rank);
                     L = v3(0, 0, 0);
                     int x, y;
-                    pixel_of(P, (uint32_t)item, chunk_s, chunk_xy0, x, y);
-                    int W = P.W, H = P.H;
+                    pixel_of(Q, (uint32_t)item, chunk_s, chunk_xy0, x, y);
+                    int W = Q.W, H = Q.H;
                     asm volatile("" : "+s"(W), "+s"(H));
                     bool ok = x < W && y < H;
                     if (ok) {
                         // primary rays from camera_kernel (or caller rays): no camera code in the loop —
                         // its uniform operands spilled 36 more SGPRs (C2 4.01 -> 3.91 ms without it)
-                        float4 r = P.rays[item];
+                        float4 r = Q.rays[item];
                         d = v3(r.x, r.y, r.z);
                         st = __float_as_uint(r.w);
-                        if (P.ray_o) {
-                            const float4 ro = P.ray_o[item];
+                        if (Q.ray_o) {
+                            const float4 ro = Q.ray_o[item];
                             o = v3(ro.x, ro.y, ro.z);
                         } else {
-                            float o0 = P.cam_o[0], o1 = P.cam_o[1], o2 = P.cam_o[2];
+                            float o0 = Q.cam_o[0], o1 = Q.cam_o[1], o2 = Q.cam_o[2];
                             asm volatile("" : "+s"(o0), "+s"(o1), "+s"(o2));
                             o = v3(o0, o1, o2);
                         }
                     }
                     if (!ok) {
-                        float* out = P.out + (size_t)item * 3;
+                        float* out = Q.out + (size_t)item * 3;
                         out[0] = 0.0f; out[1] = 0.0f; out[2] = 0.0f;
                         item = -2;
                     } else {
@@ -1800,12 +1821,16 @@ void trace_kernel_pool(TraceParams P) {
         if (item == -2) item = -1;
     };
     while (true) {
+        // the launch parameters are re-read each iteration through the kernarg pointer (scalar loads from
+        // the constant cache): kept live across the loop they exceeded the SGPR budget and were spilled
+        // into VGPR lanes, reloaded by v_readlane in every refill
+        KParams& Q = kernarg();
         // ------------------------------------------------------------------ E phase
-        refill();
+        refill(Q);
         PRT_CLOCK(4);
         if (STATS && item >= 0) book(12);
         // (a) extension traversal: every busy lane except one whose pending shadow ray ends its path
-        const bool trav = item >= 0 && !(my_sh && bounce + 1 >= P.depth);
+        const bool trav = item >= 0 && !(my_sh && bounce + 1 >= Q.depth);
         int hid = -1;
         float ht = 0.0f;
         bool hit = false;
@@ -1814,16 +1839,16 @@ void trace_kernel_pool(TraceParams P) {
             if (trav) {
                 if (STATS) { cn.ext++; cn.q0 = cn.nodes; }
                 hit = traverse_ww4<STATS, 1, Stk, false, false, true>(
-                    g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, P.fault,
-                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                    g_nodes, g_tris, o, d, kTMin, kTMax, false, stk, hid, ht, cn, nullptr, 0, Q.fault,
+                    exhausted ? 0 : Q.leaf_break, exhausted ? 0 : Q.leaf_exit, Q.guard_trips);
                 if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(0); }
-                if (!PLAIN && P.n_sph > 0) {
+                if (!PLAIN && Q.n_sph > 0) {
                     float best = hit ? ht : kTMax;
-                    for (int k = 0; k < P.n_sph; ++k) {
+                    for (int k = 0; k < Q.n_sph; ++k) {
                         float root;
-                        if (sphere_hit(P.sph[k], o, d, kTMin, best, root)) {
+                        if (sphere_hit(Q.sph[k], o, d, kTMin, best, root)) {
                             best = root;
-                            hid = P.n_tri + k;
+                            hid = Q.n_tri + k;
                             hit = true;
                         }
                     }
@@ -1847,7 +1872,7 @@ void trace_kernel_pool(TraceParams P) {
                  need && __hip_atomic_load(&ctl[9 + slot_prev], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need;
                  ++spin) {
                 if (spin >= (1u << 20)) {
-                    if (lane == 0) atomicOr(P.fault, 2);
+                    if (lane == 0) atomicOr(Q.fault, 2);
                     late = true;
                     break;
                 }
@@ -1860,8 +1885,8 @@ void trace_kernel_pool(TraceParams P) {
                 else if (r == r) L = L + pend;   // not occluded
                 my_sh = false;
                 ++bounce;
-                if (bounce >= P.depth) {
-                    float* out = P.out + (size_t)item * 3;
+                if (bounce >= Q.depth) {
+                    float* out = Q.out + (size_t)item * 3;
                     out[0] = L.x; out[1] = L.y; out[2] = L.z;
                     if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
                     item = -1;
@@ -1879,15 +1904,15 @@ void trace_kernel_pool(TraceParams P) {
                     V3 p = o + d * ht;
                     V3 ng;
                     int mid;
-                    if (PLAIN || hid < P.n_tri) {
+                    if (PLAIN || hid < Q.n_tri) {
                         float4 nm = s_nm[hid];
                         ng = xyz(nm);
                         mid = __float_as_int(nm.w);
                     } else {
                         asm volatile("");
-                        float4 sc = P.sph[hid - P.n_tri];
+                        float4 sc = Q.sph[hid - Q.n_tri];
                         ng = v3((p.x - sc.x) / sc.w, (p.y - sc.y) / sc.w, (p.z - sc.z) / sc.w);
-                        mid = P.sph_mat[hid - P.n_tri];
+                        mid = Q.sph_mat[hid - Q.n_tri];
                     }
                     const float* m = s_mats + 8 * mid;
                     const bool flip = m[4] == 0.0f && dot(ng, neg(d)) < 0.0f;
@@ -1917,12 +1942,12 @@ void trace_kernel_pool(TraceParams P) {
                             beta = beta * v3(m[0], m[1], m[2]);
                             wi = normalize(out);   // next ray (p, wi), taken up in R
                             ++bounce;
-                            if (bounce >= P.depth) finished = true;
+                            if (bounce >= Q.depth) finished = true;
                         }
                     } else if (m[3] != 0.0f) {
                         float d1 = dot(neg(d), n);
                         if (d1 > 0.0f) {
-                            V3 lc = v3(P.dl_r, P.dl_g, P.dl_b);
+                            V3 lc = v3(Q.dl_r, Q.dl_g, Q.dl_b);
                             L = bounce == 0 ? L + lc * beta : L + (lc * beta) * d1;
                         }
                         finished = true;
@@ -1931,8 +1956,8 @@ void trace_kernel_pool(TraceParams P) {
                         float u0 = rng_next(st);
                         float u1 = rng_next(st);
                         V3 l = cosine_hemisphere<true>(u0, u1);
-                        const float4* fr = s_fr + ((size_t)((PLAIN || hid < P.n_tri) ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
-                        if (PLAIN || hid < P.n_tri) {
+                        const float4* fr = s_fr + ((size_t)((PLAIN || hid < Q.n_tri) ? hid : 0) * 2 + (flip ? 1 : 0)) * 3;
+                        if (PLAIN || hid < Q.n_tri) {
                             float4 f0 = fr[0], f1 = fr[1], f2 = fr[2];
                             wi = normalize<true>(xyz(f0) * l.x + xyz(f1) * l.y + xyz(f2) * l.z);
                         } else {
@@ -1943,10 +1968,10 @@ void trace_kernel_pool(TraceParams P) {
                         float cw = dot(n, wi);
                         float dz = cw > 0.0f ? cw : 0.0f;
                         V3 ad = v3(att.x * dz, att.y * dz, att.z * dz);
-                        V3 adp = lambert_div<true>(ad, pdf, cw, P.shade_fast);
+                        V3 adp = lambert_div<true>(ad, pdf, cw, Q.shade_fast);
                         V3 nb = v3(adp.x * kInvPi, adp.y * kInvPi, adp.z * kInvPi);
                         beta = beta * nb;
-                        int li = P.n_light > 1 ? rng_int(st, 0, P.n_light - 1) : 0;
+                        int li = Q.n_light > 1 ? rng_int(st, 0, Q.n_light - 1) : 0;
                         int lo = slo[li];
                         int f = rng_int(st, 0, slo[li + 1] - lo - 1);
                         float su = sqrt_cr<true>(rng_next(st));
@@ -1976,7 +2001,7 @@ void trace_kernel_pool(TraceParams P) {
                                 V3 dd = p - p2;
                                 float sl = dot(dd, dd);
                                 V3 rad = nee_div<true>(v3(em[0] * dot1 * dot2, em[1] * dot1 * dot2, em[2] * dot1 * dot2), sl,
-                                                         dot1, dot2, P.shade_fast);
+                                                         dot1, dot2, Q.shade_fast);
                                 pend = beta * rad;
                                 pool[3 * kBlock + tid] = w.x; pool[4 * kBlock + tid] = w.y; pool[5 * kBlock + tid] = w.z;
                                 pool[6 * kBlock + tid] = t_at;
@@ -1987,7 +2012,7 @@ void trace_kernel_pool(TraceParams P) {
                             my_sh = true;
                         } else {
                             ++bounce;
-                            if (bounce >= P.depth) finished = true;
+                            if (bounce >= Q.depth) finished = true;
                         }
                     }
                     // every continuing lane parks its next ray's origin p in its pool slot (the
@@ -1996,7 +2021,7 @@ void trace_kernel_pool(TraceParams P) {
                     pool[0 * kBlock + tid] = p.x; pool[1 * kBlock + tid] = p.y; pool[2 * kBlock + tid] = p.z;
                 }
                 if (finished) {
-                    float* out = P.out + (size_t)item * 3;
+                    float* out = Q.out + (size_t)item * 3;
                     out[0] = L.x; out[1] = L.y; out[2] = L.z;
                     if (STATS && !(isfinite(L.x) && isfinite(L.y) && isfinite(L.z))) cn.nonfinite++;
                     item = -1;
@@ -2060,13 +2085,13 @@ void trace_kernel_pool(TraceParams P) {
                 float ht = 0.0f;
                 if (STATS) cn.q0 = cn.nodes;
                 bool hit = traverse_ww4<STATS, 2, Stk, false, false, true>(
-                    g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, P.fault,
-                    exhausted ? 0 : P.leaf_break, exhausted ? 0 : P.leaf_exit, P.guard_trips);
+                    g_nodes, g_tris, so, sd, kTMin, stm, true, stk, hid, ht, cn, nullptr, 0, Q.fault,
+                    exhausted ? 0 : Q.leaf_break, exhausted ? 0 : Q.leaf_exit, Q.guard_trips);
                 if (STATS) { cn.max_q = max(cn.max_q, cn.nodes - cn.q0); book_trav(4); }
-                if (!PLAIN && P.n_sph > 0 && !hit) {
-                    for (int k = 0; k < P.n_sph; ++k) {
+                if (!PLAIN && Q.n_sph > 0 && !hit) {
+                    for (int k = 0; k < Q.n_sph; ++k) {
                         float root;
-                        if (sphere_hit(P.sph[k], so, sd, kTMin, stm, root)) { hit = true; break; }
+                        if (sphere_hit(Q.sph[k], so, sd, kTMin, stm, root)) { hit = true; break; }
                     }
                 }
                 // the result travels back in the owner's t_max word: NaN = occluded
