@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=6)
     ap.add_argument("--variant", type=int, default=0, help="trace-kernel variant for every library (0 = default)")
+    ap.add_argument("--spp", type=int, default=0, help="samples per pixel instead of the config's (launch-size probes)")
     a = ap.parse_args()
     import torch
 
@@ -43,7 +44,9 @@ def main():
     from pyrenderer_amd.device_scene import DeviceScene, interleaved_tiles
     from pyrenderer_amd.flatten import flatten_scene
     N.lib()   # torch first, then the default library (one HIP runtime for all)
-    cfg = bench.CONFIGS[a.config]
+    cfg = dict(bench.CONFIGS[a.config])
+    if a.spp > 0:
+        cfg["spp"] = a.spp
     scene, camera = bench.load_scene(cfg["scene"])
     flat = flatten_scene(scene)
     cam = camera.convert_to_taichi_camera().packed()
