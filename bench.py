@@ -514,7 +514,7 @@ def main():
         # roofline of the dominant kernel (trace_kernel) on rank 0 (per launch)
         share = 1.0 / world
         n_px_rank = len(my_tiles) * T * T
-        # the variant of this workload's launches (small launches take the phase-aligned kernel)
+        # the variant of this workload's launches (DeviceScene.kernel_info: the default rule for its size)
         kinfo = ds.kernel_info(n_items=int(round(n_px_rank * args.spp / launches_per_step)))
         if args.variant:
             kinfo = dict(kinfo, variant=args.variant)

@@ -295,9 +295,8 @@ int prt_camera_rays(void* scene, const float* cam, int W, int H, int tw, int th,
  *         (7 / 8) the exact BVH4 bound its stack is sized to} */
 int prt_scene_kernel(void* scene, int32_t* out4);
 /* the same for one trace launch of n_items (pixel, sample) work items with these render flags: an
- * LDS-resident scene takes the block-pooled shadow kernel (7) for launches of at least eight items
- * per resident lane and the phase-aligned one (1) below that (config 1's 65 k samples, an 8-rank
- * shard of config 2) */
+ * LDS-resident scene whose pool fits seven blocks per CU takes the block-pooled shadow kernel (7) at
+ * every launch size (until round 6: the phase-aligned one (1) below eight items per resident lane) */
 int prt_launch_kernel(void* scene, int64_t n_items, uint32_t flags, int32_t* out4);
 /* counters of the last render call made with PRT_FLAG_STATS (synchronises) */
 int prt_last_stats(void* scene, uint64_t* stats4);

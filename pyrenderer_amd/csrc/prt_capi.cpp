@@ -278,19 +278,20 @@ bool lds_fits4(const Scene* s) {
 // kernel: 64-B quantised nodes, 16-entry LDS stack + spill, suspended traversal tails,
 // >= 6 waves/SIMD (C4: 28.6 ms at 5 waves, 27.2 at 6, 28.6 at 7 with spills).
 // An LDS-resident scene whose pooled-shadow kernel still fits seven blocks per CU takes that kernel
-// for launches of at least eight work items per resident lane (C2 4.06 vs 4.28 ms, C3 73.6 vs
-// 77.5 ms, profiles/r03/pool/); smaller launches keep the phase-aligned kernel, whose waves run
-// without block barriers: config 1's 65 k items on 459 k lanes 0.1155 vs 0.1224 ms per launch
-// (profiles/r03/c1ab/), an 8-rank shard of config 2 (2.1 M items, 3 frames in flight) 0.654 vs
-// 0.670 ms for the slowest rank (profiles/r03/shard/).
+// (C2 4.06 vs 4.28 ms, C3 73.6 vs 77.5 ms, profiles/r03/pool/) at every launch size.  Until the
+// kernarg re-reads (round 6) launches of fewer than eight items per resident lane kept the
+// phase-aligned kernel (round 3: config 1's 65 k items 0.1155 vs 0.1224 ms); with both kernels' spills
+// gone the pooled one wins there too: config 1 0.080 vs 0.094 ms per launch, config 2 at 1 / 2 / 4 spp
+// 0.245 / 0.351 / 0.490 vs 0.265 / 0.383 / 0.547 ms, the slowest of 8 single-frame shards 0.752 vs
+// 0.826 ms (3 frames in flight: 0.634 vs 0.656), profiles/r06/kernarg/variants/.
 int default_variant(const Scene* s, int64_t n_items = INT64_MAX) {
+    (void)n_items;
     if (!lds_fits4(s) || !s->stack4) return prt::kVarGlobal;
     prt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
     scene_sizes(s, P);
     P.lds_stack = s->need4;
-    const int64_t lanes = (int64_t)7 * s->cus * 256;
-    if (s->need4 <= 32 && prt::trace_smem_bytes(16, prt::kVarLdsPool, P) * 7 <= 160 * 1024 && n_items >= 8 * lanes)
+    if (s->need4 <= 32 && prt::trace_smem_bytes(16, prt::kVarLdsPool, P) * 7 <= 160 * 1024)
         return prt::kVarLdsPool;
     size_t smem = prt::trace_smem_bytes(s->stack4, prt::kVarLds, P);
     return smem * 7 <= 160 * 1024 ? prt::kVarLds : smem * 6 <= 160 * 1024 ? prt::kVarLds6 : prt::kVarLdsAnyOcc;

@@ -227,10 +227,10 @@ def _specular_scene(rough=0.0, spheres=True):
     return scene, cam, flatten_scene(scene)
 
 
-@pytest.mark.parametrize("rough,kernel", [(0.0, "default"), (0.35, "default"), (0.35, "pool")])
+@pytest.mark.parametrize("rough,kernel", [(0.0, "default"), (0.35, "default"), (0.35, "phase")])
 def test_specular_scene_matches_oracle(rough, kernel):
-    """Config 3's materials (metal, dielectric, sphere) through the C-ABI vs the oracle; "pool"
-    forces the pooled kernel (its full build: a small frame otherwise takes the phase-aligned one)."""
+    """Config 3's materials (metal, dielectric, sphere) through the C-ABI vs the oracle: the default
+    (the pooled kernel's full build) and, forced, the phase-aligned LDS kernel."""
     from pyrenderer_amd import _native as N
     from pyrenderer_amd.device_scene import DeviceScene
     scene, cam, flat = _specular_scene(rough)
@@ -238,7 +238,7 @@ def test_specular_scene_matches_oracle(rough, kernel):
     ds = DeviceScene(flat, 0)
     osc = O.OracleScene.from_flat(flat)
     c = cam.convert_to_taichi_camera().packed()
-    flags = (N.VAR_LDS_POOL << 8) if kernel == "pool" else 0
+    flags = (N.VAR_LDS << 8) if kernel == "phase" else 0
     g = _gpu_frame(ds, c, 64, 64, 4, 8, seed=4, flags=flags)
     o = osc.render(c, 64, 64, 4, 8, seed=4)
     assert np.isfinite(g).all() and g.sum() > 0
@@ -525,14 +525,13 @@ def test_mis_variant_on_the_specular_scene():
 
 
 def test_launch_size_selects_the_pooled_kernel(gpu_scene):
-    """prt_launch_kernel: on the Cornell box a large launch (config 2: 16.8 M items) takes the
-    block-pooled shadow kernel, config 1's 65 k items and an 8-rank shard of config 2 the
-    phase-aligned one (block barriers do not pay with fewer than eight items per resident lane);
-    explicit variant flags win."""
+    """prt_launch_kernel: on the Cornell box every launch takes the block-pooled shadow kernel (round 6:
+    config 1's 65 k items and an 8-rank shard of config 2 too, now that it is faster there than the
+    phase-aligned one); explicit variant flags win."""
     from pyrenderer_amd import _native as N
     assert gpu_scene.kernel_info()["variant"] == N.VAR_LDS_POOL
     assert gpu_scene.kernel_info(n_items=512 * 512 * 64)["variant"] == N.VAR_LDS_POOL
-    assert gpu_scene.kernel_info(n_items=128 * 128 * 4)["variant"] == N.VAR_LDS
-    assert gpu_scene.kernel_info(n_items=512 * 512 * 64 // 8)["variant"] == N.VAR_LDS   # an 8-rank shard
-    assert gpu_scene.kernel_info(n_items=128 * 128 * 4, flags=N.VAR_LDS_POOL << 8)["variant"] == N.VAR_LDS_POOL
+    assert gpu_scene.kernel_info(n_items=128 * 128 * 4)["variant"] == N.VAR_LDS_POOL
+    assert gpu_scene.kernel_info(n_items=512 * 512 * 64 // 8)["variant"] == N.VAR_LDS_POOL   # an 8-rank shard
+    assert gpu_scene.kernel_info(n_items=128 * 128 * 4, flags=N.VAR_LDS << 8)["variant"] == N.VAR_LDS
     assert gpu_scene.kernel_info(n_items=512 * 512 * 64, flags=N.PRT_FLAG_MIS_NEE)["variant"] == N.VAR_MIS[0]
